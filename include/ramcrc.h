@@ -1,0 +1,147 @@
+/*
+ * ramcrc.h -- the C ABI of the MI355X-native CRC32C path (libramcrc.so).
+ *
+ * Plain C: no HIP, ROCm or torch types.  Device pointers are `const void*` /
+ * `uint32_t*` into memory the caller allocated on the GPU; streams are passed
+ * as `void*` (a hipStream_t; NULL = the legacy default stream).
+ *
+ * Semantics of every CRC entry point follow RAMCloud's Crc32C
+ * (/root/reference/src/Crc32C.h):
+ *   state 0xFFFFFFFF at construction            (src/Crc32C.h:175-179)
+ *   update(p, n): state = CRC32C step, no ~      (src/Crc32C.h:200-206)
+ *   getResult():  ~state, state unchanged        (src/Crc32C.h:247-249)
+ * The batch entry points compute, for every buffer i,
+ *   state_i = init ? init[i] : 0xFFFFFFFF;  state_i = update(buf_i, len_i)
+ *   out[i]  = (flags & RAMCRC_FINALIZE) ? ~state_i : state_i
+ * i.e. exactly `Crc32C c; c.result = init[i]; c.update(buf_i, len_i);`
+ * followed by getResult() or a read of c.result.
+ *
+ * Errors: every int-returning function returns RAMCRC_OK (0) or a negative
+ * code; nothing throws across this boundary.  The reference's update() cannot
+ * fail (src/Crc32C.h:200-206); integrity failures stay with the caller, who
+ * compares the returned per-buffer CRCs (src/Segment.cc:793-797).
+ */
+#ifndef RAMCRC_H
+#define RAMCRC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    RAMCRC_OK = 0,
+    RAMCRC_EINVAL = -1,   /* bad argument (null pointer, size overflow) */
+    RAMCRC_ENOMEM = -2,   /* device or pinned allocation failed */
+    RAMCRC_EHIP = -3,     /* a HIP runtime call failed; see ramcrc_last_hip_error */
+    RAMCRC_ENODEV = -4,   /* no usable gfx950 device */
+    RAMCRC_ERCCL = -5     /* RCCL failure (multi-GPU shard) */
+};
+
+/* Output flag: apply the final inversion (Crc32C::getResult, src/Crc32C.h:247).
+ * Without it the raw running state (Crc32C::result, :259) is returned, which
+ * callers use to keep chaining (src/LogDigest.cc:75-80, src/Segment.cc:677-681). */
+#define RAMCRC_FINALIZE 1u
+
+/* ---------------------------------------------------------------- host --- */
+
+/* Replaces the body of Crc32C::update(const void*, uint32_t)
+ * (src/Crc32C.h:200-206) when useHardware: SSE4.2 crc32 instruction,
+ * three interleaved streams recombined with X^n operators.  Same result as
+ * intelCrc32C (src/Crc32C.h:39-93) for every input.  64-bit length
+ * (the reference takes uint32_t; see SURVEY.md section 7, hard part 6). */
+uint32_t ramcrc_update_hw(uint32_t state, const void* data, uint64_t nbytes);
+
+/* Replaces softwareCrc32C (src/Crc32C.h:96-153): slicing-by-8, tables
+ * generated from the polynomial.  Used when forceSoftware or no SSE4.2. */
+uint32_t ramcrc_update_sw(uint32_t state, const void* data, uint64_t nbytes);
+
+/* Best available host path (what Crc32C::update uses by default). */
+uint32_t ramcrc_update(uint32_t state, const void* data, uint64_t nbytes);
+
+/* Replaces haveSse42()/Crc32C::haveHardware (src/Crc32C.cc:24-45):
+ * 1 if this CPU and build support the crc32 instruction. */
+int ramcrc_cpu_has_hw(void);
+
+/* State algebra.  ramcrc_shift(s, n) is the
+ * state reached from s by updating with n zero bytes; ramcrc_combine(a, b, n)
+ * = raw state of A||B given a = raw(0-based) state after A and b = raw(0, B)
+ * with n = |B|.  Both are exact GF(2) identities. */
+uint32_t ramcrc_shift(uint32_t state, uint64_t nbytes);
+uint32_t ramcrc_combine(uint32_t raw_a, uint32_t raw_b, uint64_t len_b);
+
+/* -------------------------------------------------------------- device --- */
+
+typedef struct ramcrc_ctx ramcrc_ctx;
+
+/* Creates a context bound to HIP device `device` (scratch buffers, pinned
+ * staging, device properties).  No GPU work happens at static-init time;
+ * contexts are created lazily by callers.  A context serialises its own
+ * scratch: use one context per concurrently-launching thread/stream. */
+int ramcrc_ctx_create(int device, ramcrc_ctx** out);
+int ramcrc_ctx_destroy(ramcrc_ctx* ctx);
+
+/* Pre-size device scratch so later launches never allocate (required before
+ * capturing launches into a hipGraph).  max_chunks = number of 256 KiB chunks
+ * a launch may cover; max_entries = entries of the largest batch call. */
+int ramcrc_ctx_reserve(ramcrc_ctx* ctx, uint64_t max_chunks, uint64_t max_entries);
+
+/* Uniform contiguous segments (the recovery-scan batch, src/BackupMasterRecovery.cc:743-809
+ * per replica): segment i = d_base + i*seg_bytes, i < nseg.  d_init may be NULL.
+ * Stream-ordered, asynchronous. */
+int ramcrc_segments_device(ramcrc_ctx* ctx, const void* d_base, uint64_t seg_bytes,
+                           uint64_t nseg, const uint32_t* d_init, uint32_t* d_out,
+                           uint32_t flags, void* stream);
+
+/* General batch: buffer i = d_base + d_off[i], length d_len[i] (64-bit, any
+ * alignment, any length including 0).  Buffers of >= 64 KiB are split into
+ * 256 KiB chunks scanned by all CUs; smaller ones go to the small-entry
+ * kernel.  Stream-ordered, asynchronous. */
+int ramcrc_batch_device(ramcrc_ctx* ctx, const void* d_base, const uint64_t* d_off,
+                        const uint64_t* d_len, const uint32_t* d_init, uint32_t* d_out,
+                        uint64_t n, uint32_t flags, void* stream);
+
+/* Small-entry path only (log entries / objects, src/ObjectManager.cc:659-669):
+ * every buffer through the per-entry kernel regardless of length. */
+int ramcrc_entries_device(ramcrc_ctx* ctx, const void* d_base, const uint64_t* d_off,
+                          const uint64_t* d_len, const uint32_t* d_init, uint32_t* d_out,
+                          uint64_t n, uint32_t flags, void* stream);
+
+/* Host buffers in, host CRCs out (segments arriving from disk/NIC buffers,
+ * src/BackupStorage.h:227): pinned staging + H2D + kernel + D2H, synchronous.
+ * ptrs[i]/lens[i] describe buffer i; init may be NULL. */
+int ramcrc_batch_host(ramcrc_ctx* ctx, const void* const* ptrs, const uint64_t* lens,
+                      const uint32_t* init, uint32_t* out, uint64_t n, uint32_t flags);
+
+/* Streaming segments host-to-host with H2D on a copy stream overlapped with
+ * kernels on a compute stream (BASELINE config 5).  Segment i = h_base +
+ * i*seg_bytes (host memory, pinned or pageable); CRCs to h_out.  Uses up to
+ * `depth` in-flight device slots of `batch` segments each. */
+int ramcrc_stream_host(ramcrc_ctx* ctx, const void* h_base, uint64_t seg_bytes,
+                       uint64_t nseg, uint32_t* h_out, uint32_t flags, int batch, int depth);
+
+/* Kernel timing (for benchmarks): when enabled, every launch brackets its
+ * byte-scan kernel (k_chunks, or k_entries on the small path) with HIP events
+ * on the launch stream.  ramcrc_ctx_scan_time waits for the recorded events,
+ * returns the summed kernel milliseconds and the number of bracketed launches
+ * since the last call, and resets both. */
+int ramcrc_ctx_set_timing(ramcrc_ctx* ctx, int enable);
+int ramcrc_ctx_scan_time(ramcrc_ctx* ctx, double* total_ms, uint64_t* launches);
+
+/* Nonzero if a planned launch found more chunks than the context's scratch
+ * holds (its outputs were not written); raise ramcrc_ctx_reserve.  Synchronous. */
+int ramcrc_ctx_status(ramcrc_ctx* ctx, uint32_t* status);
+
+/* Diagnostics. */
+const char* ramcrc_strerror(int code);
+int ramcrc_last_hip_error(void);            /* last hipError_t seen (thread-local) */
+int ramcrc_device_count(void);
+const char* ramcrc_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RAMCRC_H */

@@ -1,0 +1,159 @@
+"""ORACLE -- TEST INFRASTRUCTURE ONLY.
+
+ctypes bindings for the CPU restatement (oracle/liboracle.so) and, when it has
+been built, the reference's own compiled hardware path
+(oracle/_ref/libref_crc32c.so).  Imported only by tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg -- never by the ramcloud_amd product path.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+REF_PATH = os.path.join(HERE, "_ref", "libref_crc32c.so")
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+
+IMPL_SSE42, IMPL_SLICING8, IMPL_BITWISE = 0, 1, 2
+
+_lib = None
+_ref = None
+
+
+def build(with_ref=None):
+    """Compile the oracle (and the reference harness when /root/reference exists)."""
+    subprocess.check_call(["make", "-s", "-C", HERE, "liboracle.so"])
+    if with_ref is None:
+        with_ref = os.path.isdir("/root/reference/src")
+    if with_ref:
+        subprocess.check_call(["make", "-s", "-C", HERE, "ref"])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build(with_ref=False)
+        L = ctypes.CDLL(LIB_PATH)
+        for name in ("oracle_bitwise", "oracle_slicing8", "oracle_sse42"):
+            f = getattr(L, name)
+            f.restype = ctypes.c_uint32
+            f.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64]
+        L.oracle_mulmod.restype = ctypes.c_uint32
+        L.oracle_mulmod.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+        L.oracle_xpow8.restype = ctypes.c_uint32
+        L.oracle_xpow8.argtypes = [ctypes.c_uint64]
+        L.oracle_shift.restype = ctypes.c_uint32
+        L.oracle_shift.argtypes = [ctypes.c_uint32, ctypes.c_uint64]
+        L.oracle_splitmix_fill.restype = None
+        L.oracle_splitmix_fill.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64]
+        L.oracle_entries.restype = None
+        L.oracle_entries.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                     ctypes.c_int, ctypes.c_int]
+        L.oracle_segments_mt.restype = ctypes.c_int
+        L.oracle_segments_mt.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                         ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.oracle_have_sse42.restype = ctypes.c_int
+        L.oracle_init()
+        _lib = L
+    return _lib
+
+
+def ref_available():
+    return os.path.exists(REF_PATH)
+
+
+def ref():
+    """The reference's own intelCrc32C (src/Crc32C.h:39-93), or None if not built."""
+    global _ref
+    if _ref is None and ref_available():
+        R = ctypes.CDLL(REF_PATH)
+        R.ref_intel_crc32c.restype = ctypes.c_uint32
+        R.ref_intel_crc32c.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64]
+        R.ref_segments_mt.restype = ctypes.c_int
+        R.ref_segments_mt.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                      ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        _ref = R
+    return _ref
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def _as_u8(data):
+    if isinstance(data, (bytes, bytearray)):
+        return np.frombuffer(bytes(data), dtype=np.uint8)
+    return np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+
+
+def crc_raw(state, data, impl=IMPL_SSE42):
+    """Crc32C with result=state, update(data): the raw (pre-inversion) state."""
+    buf = _as_u8(data)
+    f = (lib().oracle_sse42, lib().oracle_slicing8, lib().oracle_bitwise)[impl]
+    return int(f(state & 0xFFFFFFFF, _ptr(buf), buf.size))
+
+
+def crc32c(data, impl=IMPL_SSE42):
+    """Crc32C().update(data).getResult()."""
+    return (~crc_raw(0xFFFFFFFF, data, impl)) & 0xFFFFFFFF
+
+
+def ref_crc_raw(state, data):
+    R = ref()
+    buf = _as_u8(data)
+    return int(R.ref_intel_crc32c(state & 0xFFFFFFFF, _ptr(buf), buf.size))
+
+
+def mulmod(a, b):
+    return int(lib().oracle_mulmod(a & 0xFFFFFFFF, b & 0xFFFFFFFF))
+
+
+def xpow8(n):
+    return int(lib().oracle_xpow8(n))
+
+
+def shift(state, nbytes):
+    return int(lib().oracle_shift(state & 0xFFFFFFFF, nbytes))
+
+
+def splitmix_bytes(seed, nbytes):
+    out = np.empty(nbytes, dtype=np.uint8)
+    lib().oracle_splitmix_fill(seed & 0xFFFFFFFFFFFFFFFF, _ptr(out), nbytes)
+    return out
+
+
+def entries(base, off, length, init=None, finalize=True, impl=IMPL_SSE42):
+    base = _as_u8(base)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    length = np.ascontiguousarray(length, dtype=np.uint64)
+    n = off.size
+    if n and int((off + length).max()) > base.size:
+        raise ValueError("entry past end of base buffer")
+    out = np.empty(n, dtype=np.uint32)
+    init_a = None if init is None else np.ascontiguousarray(init, dtype=np.uint32)
+    lib().oracle_entries(_ptr(base), _ptr(off), _ptr(length), _ptr(init_a), _ptr(out),
+                         n, 1 if finalize else 0, impl)
+    return out
+
+
+def segments(base, seg_bytes, nseg, threads=1, impl=IMPL_SSE42, pin=True, use_ref=False):
+    """getResult() of each whole segment; threads take segments round-robin."""
+    base = _as_u8(base)
+    if base.size < seg_bytes * nseg:
+        raise ValueError("base buffer too small")
+    out = np.empty(nseg, dtype=np.uint32)
+    if use_ref:
+        rc = ref().ref_segments_mt(_ptr(base), seg_bytes, nseg, _ptr(out), threads, 1 if pin else 0)
+    else:
+        rc = lib().oracle_segments_mt(_ptr(base), seg_bytes, nseg, _ptr(out), threads, impl,
+                                      1 if pin else 0)
+    if rc != 0:
+        raise RuntimeError("thread start failed")
+    return out

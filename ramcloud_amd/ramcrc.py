@@ -1,0 +1,235 @@
+"""Python binding of libramcrc (include/ramcrc.h) -- the product path.
+
+The CRC work happens in the HIP kernels of libramcrc.so; this module only
+passes pointers.  There is no CPU fallback for the device entry points: if the
+library is missing or a call fails, an exception is raised.
+
+Device memory and streams come from PyTorch (plumbing only): tensors are
+passed by data_ptr(), streams by torch.cuda.current_stream().cuda_stream.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import build as _build
+
+_c = ctypes
+_lib = None
+
+FINALIZE = 1
+
+_ERRORS = {0: "ok", -1: "invalid argument", -2: "out of memory", -3: "HIP error",
+           -4: "no usable device", -5: "RCCL error"}
+
+
+class RamcrcError(RuntimeError):
+    pass
+
+
+def lib_path():
+    return _build.LIB
+
+
+def lib():
+    """Load libramcrc.so; raises if it has not been built (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = _build.LIB
+    if not os.path.exists(path):
+        raise RamcrcError(f"libramcrc.so not built ({path}); run python -m ramcloud_amd.build")
+    L = _c.CDLL(path)
+    vp, u32, u64, i32 = _c.c_void_p, _c.c_uint32, _c.c_uint64, _c.c_int
+    sig = {
+        "ramcrc_update_hw": (u32, [u32, vp, u64]),
+        "ramcrc_update_sw": (u32, [u32, vp, u64]),
+        "ramcrc_update": (u32, [u32, vp, u64]),
+        "ramcrc_cpu_has_hw": (i32, []),
+        "ramcrc_shift": (u32, [u32, u64]),
+        "ramcrc_combine": (u32, [u32, u32, u64]),
+        "ramcrc_ctx_create": (i32, [i32, _c.POINTER(vp)]),
+        "ramcrc_ctx_destroy": (i32, [vp]),
+        "ramcrc_ctx_reserve": (i32, [vp, u64, u64]),
+        "ramcrc_segments_device": (i32, [vp, vp, u64, u64, vp, vp, u32, vp]),
+        "ramcrc_batch_device": (i32, [vp, vp, vp, vp, vp, vp, u64, u32, vp]),
+        "ramcrc_entries_device": (i32, [vp, vp, vp, vp, vp, vp, u64, u32, vp]),
+        "ramcrc_batch_host": (i32, [vp, vp, vp, vp, vp, u64, u32]),
+        "ramcrc_stream_host": (i32, [vp, vp, u64, u64, vp, u32, i32, i32]),
+        "ramcrc_ctx_set_timing": (i32, [vp, i32]),
+        "ramcrc_ctx_scan_time": (i32, [vp, _c.POINTER(_c.c_double), _c.POINTER(u64)]),
+        "ramcrc_ctx_status": (i32, [vp, _c.POINTER(u32)]),
+        "ramcrc_strerror": (_c.c_char_p, [i32]),
+        "ramcrc_last_hip_error": (i32, []),
+        "ramcrc_device_count": (i32, []),
+        "ramcrc_build_info": (_c.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def exported_symbols():
+    return [n for n in dir(lib()) if n.startswith("ramcrc_")]
+
+
+def _check(rc, what):
+    if rc != 0:
+        msg = lib().ramcrc_strerror(rc).decode()
+        raise RamcrcError(f"{what} failed: {_ERRORS.get(rc, rc)} ({msg})")
+
+
+def _buf(data):
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        a = np.frombuffer(bytes(data), dtype=np.uint8)
+    else:
+        a = np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+    return a, _c.c_void_p(a.ctypes.data)
+
+
+# ------------------------------------------------------------------ host
+def update(state, data):
+    """Crc32C::update on the host hardware path; returns the raw state."""
+    a, p = _buf(data)
+    return int(lib().ramcrc_update(state & 0xFFFFFFFF, p, a.size))
+
+
+def update_sw(state, data):
+    a, p = _buf(data)
+    return int(lib().ramcrc_update_sw(state & 0xFFFFFFFF, p, a.size))
+
+
+def update_hw(state, data):
+    a, p = _buf(data)
+    return int(lib().ramcrc_update_hw(state & 0xFFFFFFFF, p, a.size))
+
+
+def crc32c(data):
+    """Crc32C().update(data).getResult() on the host."""
+    return (~update(0xFFFFFFFF, data)) & 0xFFFFFFFF
+
+
+def shift(state, nbytes):
+    return int(lib().ramcrc_shift(state & 0xFFFFFFFF, nbytes))
+
+
+def combine(raw_a, raw_b, len_b):
+    return int(lib().ramcrc_combine(raw_a & 0xFFFFFFFF, raw_b & 0xFFFFFFFF, len_b))
+
+
+def cpu_has_hw():
+    return bool(lib().ramcrc_cpu_has_hw())
+
+
+def device_count():
+    return int(lib().ramcrc_device_count())
+
+
+# ---------------------------------------------------------------- device
+def _ptr(t):
+    if t is None:
+        return None
+    if isinstance(t, int):
+        return _c.c_void_p(t)
+    return _c.c_void_p(t.data_ptr())
+
+
+def _stream(stream):
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream()
+    if isinstance(stream, int):
+        return _c.c_void_p(stream)
+    return _c.c_void_p(stream.cuda_stream)
+
+
+class Context:
+    """A libramcrc context on one GPU (scratch + staging).  One per stream/thread."""
+
+    def __init__(self, device=0):
+        h = _c.c_void_p()
+        _check(lib().ramcrc_ctx_create(int(device), _c.byref(h)), "ramcrc_ctx_create")
+        self._h = h
+        self.device = int(device)
+
+    def close(self):
+        if self._h:
+            lib().ramcrc_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_timing(self, enable=True):
+        _check(lib().ramcrc_ctx_set_timing(self._h, 1 if enable else 0), "ramcrc_ctx_set_timing")
+
+    def scan_time(self):
+        """(summed scan-kernel milliseconds, launches) since the last call."""
+        ms = _c.c_double(0)
+        n = _c.c_uint64(0)
+        _check(lib().ramcrc_ctx_scan_time(self._h, _c.byref(ms), _c.byref(n)), "ramcrc_ctx_scan_time")
+        return ms.value, n.value
+
+    def status(self):
+        s = _c.c_uint32(0)
+        _check(lib().ramcrc_ctx_status(self._h, _c.byref(s)), "ramcrc_ctx_status")
+        return s.value
+
+    def reserve(self, max_chunks, max_entries):
+        _check(lib().ramcrc_ctx_reserve(self._h, max_chunks, max_entries), "ramcrc_ctx_reserve")
+
+    # All tensors below are CUDA tensors; outputs are int32 tensors holding the
+    # uint32 CRC bit patterns.
+    def segments(self, data, seg_bytes, nseg, out, init=None, finalize=True, stream=None):
+        rc = lib().ramcrc_segments_device(self._h, _ptr(data), seg_bytes, nseg, _ptr(init),
+                                          _ptr(out), FINALIZE if finalize else 0, _stream(stream))
+        _check(rc, "ramcrc_segments_device")
+        return out
+
+    def batch(self, data, off, length, out, init=None, finalize=True, stream=None):
+        n = off.numel()
+        rc = lib().ramcrc_batch_device(self._h, _ptr(data), _ptr(off), _ptr(length), _ptr(init),
+                                       _ptr(out), n, FINALIZE if finalize else 0, _stream(stream))
+        _check(rc, "ramcrc_batch_device")
+        return out
+
+    def entries(self, data, off, length, out, init=None, finalize=True, stream=None):
+        n = off.numel()
+        rc = lib().ramcrc_entries_device(self._h, _ptr(data), _ptr(off), _ptr(length), _ptr(init),
+                                         _ptr(out), n, FINALIZE if finalize else 0, _stream(stream))
+        _check(rc, "ramcrc_entries_device")
+        return out
+
+    def batch_host(self, buffers, init=None, finalize=True):
+        """CRC a list of host buffers (bytes / numpy) on the GPU; returns np.uint32."""
+        arrs = [_buf(b)[0] for b in buffers]
+        n = len(arrs)
+        ptrs = (_c.c_void_p * max(n, 1))(*[a.ctypes.data for a in arrs])
+        lens = np.array([a.size for a in arrs], dtype=np.uint64)
+        out = np.zeros(n, dtype=np.uint32)
+        init_a = None if init is None else np.ascontiguousarray(init, dtype=np.uint32)
+        rc = lib().ramcrc_batch_host(self._h, ptrs, _c.c_void_p(lens.ctypes.data),
+                                     None if init_a is None else _c.c_void_p(init_a.ctypes.data),
+                                     _c.c_void_p(out.ctypes.data), n,
+                                     FINALIZE if finalize else 0)
+        _check(rc, "ramcrc_batch_host")
+        return out
+
+    def stream_host(self, host_segments, seg_bytes, nseg, finalize=True, batch=8, depth=3):
+        """Host-to-host streaming CRC (config 5).  host_segments: numpy uint8 or a
+        pinned torch CPU tensor; returns np.uint32[nseg]."""
+        out = np.zeros(nseg, dtype=np.uint32)
+        if hasattr(host_segments, "data_ptr"):
+            base = _c.c_void_p(host_segments.data_ptr())
+        else:
+            base = _c.c_void_p(np.ascontiguousarray(host_segments).ctypes.data)
+        rc = lib().ramcrc_stream_host(self._h, base, seg_bytes, nseg, _c.c_void_p(out.ctypes.data),
+                                      FINALIZE if finalize else 0, batch, depth)
+        _check(rc, "ramcrc_stream_host")
+        return out

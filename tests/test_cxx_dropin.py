@@ -1,0 +1,30 @@
+"""Compile and run tests/cpp/crc32c_test.cc: the drop-in include/ramcloud/Crc32C.h
+used exactly as RAMCloud's callers and src/Crc32CTest.cc use the reference class."""
+import os
+import subprocess
+
+from conftest import ROOT
+
+
+def test_cxx_dropin(golden, ramcrc, tmp_path):
+    vec = tmp_path / "vectors.txt"
+    with open(vec, "w") as f:
+        f.write("INPUT " + bytes(golden["crc32c_test"]["input"]).hex() + "\n")
+        for c in golden["crc32c_test"]["crcByLength"]:
+            f.write(f"CRC {c:08x}\n")
+        for c in golden["segment_certificates"] + golden["object_checksums"]:
+            data = c.get("stream", c.get("bytes"))
+            f.write(f"GOLDEN {data} {c['checksum']:08x}\n")
+    exe = tmp_path / "crc32c_test"
+    libdir = os.path.dirname(ramcrc.lib_path())
+    cmd = ["g++", "-std=c++11", "-O2", "-Wall", "-Werror",
+           "-I" + os.path.join(ROOT, "tests", "cpp"),
+           "-I" + os.path.join(ROOT, "include", "ramcloud"),
+           "-I" + os.path.join(ROOT, "include"),
+           os.path.join(ROOT, "tests", "cpp", "crc32c_test.cc"),
+           os.path.join(ROOT, "ramcloud_amd", "dropin", "Crc32C.cc"),
+           "-L" + libdir, "-lramcrc", "-Wl,-rpath," + libdir, "-o", str(exe)]
+    subprocess.check_call(cmd)
+    out = subprocess.run([str(exe), str(vec)], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "failures=0" in out.stdout
