@@ -203,7 +203,7 @@ def main():
         kat_ok = None
         if rank == 0 and r["first_seed"] == workloads.SEGMENT_SEED:
             with open(os.path.join(ROOT, "tests", "golden", "crc32c_golden.json")) as f:
-                kats = {k["name"]: k["crc"] for k in json.load(f)["kat"]}
+                kats = {k["name"]: k["crc"] for k in json.load(f)["kat"] if "crc" in k}
             kat_ok = all(int(r["local_crcs"][i]) == kats[f"bench_segment_{i}"]
                          for i in range(min(4, r["nseg"])))
         line = None

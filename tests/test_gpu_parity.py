@@ -113,7 +113,7 @@ def test_segments_aligned_kats(ctx, golden, oracle_mod):
     out = torch.zeros(nseg, dtype=torch.int32, device="cuda")
     ctx.segments(data, 8 * MiB, nseg, out)
     got = u32(out)
-    kats = {k["name"]: k["crc"] for k in golden["kat"]}
+    kats = {k["name"]: k["crc"] for k in golden["kat"] if "crc" in k}
     for i in range(4):
         assert got[i] == kats[f"bench_segment_{i}"], i
     host = data.cpu().numpy()
