@@ -45,7 +45,7 @@ def build(force=False, verbose=False):
     os.makedirs(LIBDIR, exist_ok=True)
     tmp = LIB + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-fconstexpr-steps=200000000", "-Wall", "-Wno-unused-function",
+           "-fconstexpr-steps=1000000000", "-Wall", "-Wno-unused-function",
            "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
     cmd += [os.path.join(CSRC, s) for s in SOURCES]
     cmd += ["-o", tmp]

@@ -66,18 +66,20 @@ constexpr int kUnroll = 8;                         // blocks in flight per wave
 // ------------------------------------------------------------------ tables
 struct DeviceTables {
     OpTable stride_large;   // X^1024: Horner step of k_chunks
-    OpTable stride_small;   // X^16:   Horner step of k_entries
+    OpTable stride_small;   // X^128:  Horner step of k_entries (8 lanes x 16 B)
     OpTable comb[7];        // X^4, X^16, X^32, X^64, X^128, X^256, X^512
     ramcrc::ByteTable t0;   // X^1 byte step
     uint32_t xblk[4][256];  // x^(8 * 1024 * b * 256^j)
     uint32_t xinv[1024];    // x^(-8 p)
+    uint32_t ecst[8][128];  // k_entries: x^(8 (16 (7 - l) - pad)), lane l of a group
+    uint32_t pos[129][256]; // k_entries_tiny: X^m(byte) for m = 0..128
 };
 
 constexpr DeviceTables make_device_tables()
 {
     DeviceTables t{};
     t.stride_large = ramcrc::make_op(kBlock);
-    t.stride_small = ramcrc::make_op(16);
+    t.stride_small = ramcrc::make_op(128);
     const uint64_t comb_d[7] = {4, 16, 32, 64, 128, 256, 512};
     for (int i = 0; i < 7; i++)
         t.comb[i] = ramcrc::make_op(comb_d[i]);
@@ -96,6 +98,16 @@ constexpr DeviceTables make_device_tables()
         t.xinv[p] = acc;
         acc = ramcrc::mulmod(acc, inv8);
     }
+    for (int m = 0; m <= 128; m++) {
+        const uint32_t c = ramcrc::xpow8(uint64_t(m));
+        for (uint32_t b = 0; b < 256; b++)
+            t.pos[m][b] = ramcrc::mulmod(b, c);
+    }
+    for (int l = 0; l < 8; l++)
+        for (int pad = 0; pad < 128; pad++) {
+            const int d = 16 * (7 - l) - pad;
+            t.ecst[l][pad] = ramcrc::mulmod(t.xinv[d < 0 ? -d : 0], ramcrc::xpow8(d > 0 ? d : 0));
+        }
     return t;
 }
 
@@ -115,8 +127,10 @@ constexpr uint32_t kRepBytes = 131072;
 constexpr uint32_t kCombOff = kRepBytes;                  // k_chunks: 7 x 4 KiB
 constexpr uint32_t kLdsChunks = kCombOff + 7 * 4096;      // 159744 B
 constexpr uint32_t kX4Off = kRepBytes;                    // k_entries: X^4 (4 KiB)
-constexpr uint32_t kT0Off = kRepBytes + 4096;             // k_entries: X^1 (1 KiB)
-constexpr uint32_t kLdsEntries = kT0Off + 1024;           // 136192 B
+constexpr uint32_t kCstOff = kX4Off + 4096;               // k_entries: ecst (4 KiB)
+constexpr uint32_t kT0Off = kCstOff + 4096;               // k_entries: X^1 (1 KiB)
+constexpr uint32_t kBinOff = kT0Off + 1024;               // k_entries: bin table (4 KiB)
+constexpr uint32_t kLdsEntries = kBinOff + 4096;          // 143360 B
 static_assert(kLdsChunks <= 160 * 1024, "LDS budget");
 
 __device__ __forceinline__ void fill_replicated(uint8_t* lds, const OpTable& op)
@@ -212,17 +226,18 @@ __device__ __forceinline__ uint32_t xpow_blocks(uint64_t t)
 __device__ __forceinline__ uint32_t fix_word(uint32_t w, uint64_t a, uint64_t S, uint64_t E,
                                              uint32_t init)
 {
-    const int64_t dlo = int64_t(S) - int64_t(a);
-    const int64_t dhi = int64_t(E) - int64_t(a);
-    const int lo = dlo <= 0 ? 0 : (dlo >= 4 ? 4 : int(dlo));
-    const int hi = dhi <= 0 ? 0 : (dhi >= 4 ? 4 : int(dhi));
-    const uint32_t mhi = hi >= 4 ? 0xFFFFFFFFu : ((1u << (8 * hi)) - 1u);
-    const uint32_t mlo = lo >= 4 ? 0xFFFFFFFFu : ((1u << (8 * lo)) - 1u);
-    w &= (hi > lo) ? (mhi & ~mlo) : 0u;
-    const int64_t d = -dlo;  // a - S
-    if (d > -4 && d < 4)
-        w ^= d >= 0 ? (init >> (8 * int(d))) : (init << (8 * int(-d)));
-    return w;
+    // Branch-free.  ds/de: byte offsets of S and E from this word, clamped.
+    const int64_t ds64 = int64_t(S - a), de64 = int64_t(E - a);
+    const int ds = ds64 < -8 ? -8 : (ds64 > 8 ? 8 : int(ds64));
+    const int de = de64 < -8 ? -8 : (de64 > 8 ? 8 : int(de64));
+    const int lo = min(max(ds, 0), 4), hi = min(max(de, 0), 4);
+    const uint32_t mhi = uint32_t((1ull << (8 * hi)) - 1);
+    const uint32_t mlo = uint32_t((1ull << (8 * lo)) - 1);
+    w &= mhi & ~mlo;
+    // init occupies bytes S..S+3; word byte q holds init byte q - ds
+    const int dd = -ds;   // a - S
+    const uint32_t inj = uint32_t((uint64_t(init) << 24) >> (24 + 8 * (dd < -3 ? -3 : (dd > 3 ? 3 : dd))));
+    return w ^ ((dd > -4 && dd < 4) ? inj : 0u);
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -502,57 +517,500 @@ __global__ __launch_bounds__(256) void k_combine(BatchDesc d, Plan pl, uint64_t 
 }
 
 // ------------------------------------------------------------ k_entries
-template <int kMode>
-__global__ __launch_bounds__(kThreads, 1) void k_entries(BatchDesc d, int skip_large)
-{
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsEntries];
-    fill_replicated(lds, g_tab.stride_small);
-    fill_plain(lds, kX4Off, &g_tab.comb[0].t[0][0], 1024);
-    fill_plain(lds, kT0Off, g_tab.t0.t, 256);
-    __syncthreads();
+// Small buffers (log entries, objects; src/ObjectManager.cc:659-669).  A
+// group of 8 lanes owns one entry and reads it as 128-byte steps (lane l: 16
+// bytes at A + 128 k + 16 l, A = S rounded down to 16): groups of 8 lanes
+// reading 128 contiguous bytes stream at the full HBM rate on gfx950 (7.05
+// TB/s measured, profiles/r01/membench_access_patterns.txt), while one lane
+// per entry reaches only 2 TB/s.  Horner with X^128 per step through the
+// replicated LDS tables; at the end the four slot accumulators fold with
+// X^4, one GF(2) multiply by x^(8 (16 (7-l) - pad)) moves each lane's partial
+// to the entry end (pad = zero bytes past E in the last step), and three
+// shuffles XOR the group.  Entries are first binned by step count
+// (k_bin_*) so the 8 groups of a wave finish together; bins of at most 8
+// steps batch several entry octets per load round.
+constexpr int kG = 8;                      // lanes per entry group
+constexpr uint64_t kStep = kG * 16;        // bytes per group step
+constexpr int kNB = 161;                   // step-count bins
+constexpr int kEU = 8;                     // steps per load round (batched bins)
+constexpr int kPU = 4;                     // ping-pong depth (pipelined bins)
+constexpr uint32_t kNoIdx = 0xFFFFFFFFu;   // empty slot
+constexpr uint64_t kOctetCost = 3;         // per-octet overhead in step units (work split)
+constexpr uint32_t kLdsTiny = 129 * 1024;  // k_entries_tiny: X^m(byte), m = 0..128
 
-    const int lane = threadIdx.x & (kWaveSize - 1);
-    const RepOp op(lane);
-    const uint32_t* t0 = reinterpret_cast<const uint32_t*>(lds + kT0Off);
+struct BinTable {
+    uint64_t start[kNB];      // first sorted slot of the bin (multiple of 8)
+    uint64_t count[kNB];      // entries in the bin
+    uint64_t items[kNB + 1];  // exclusive prefix of octets * kmax: work units
+    uint64_t cursor[kNB];     // scatter cursors
+    uint32_t hist[kNB];       // entry counts; zero between launches
+};
+
+struct Sorted {
+    BinTable* bt;
+    u32x4* desc;       // {S lo, S hi, E lo, E hi} per sorted slot
+    uint32_t* idx;     // original index; kNoIdx for padding slots
+    uint32_t* init;    // initial state per sorted slot (when the batch has one)
+};
+
+__device__ __forceinline__ uint64_t entry_steps(uint64_t S, uint64_t E)
+{
+    return (E - (S & ~uint64_t(15)) + kStep - 1) / kStep;
+}
+
+// Bin 0: n < 4 (bytewise).  Bins 1..32: exactly that many steps.  Above:
+// four bins per octave of the step count.
+__device__ __forceinline__ int bin_of(uint64_t S, uint64_t E)
+{
+    if (E - S < 4)
+        return 0;
+    const uint64_t K = entry_steps(S, E);
+    if (K <= 32)
+        return int(K);
+    const int m = 63 - __builtin_clzll(K);
+    return 33 + 4 * (m - 5) + int((K >> (m - 2)) & 3);
+}
+
+__device__ __forceinline__ uint64_t bin_kmax(int b)
+{
+    if (b <= 32)
+        return b == 0 ? 1 : uint64_t(b);
+    const int m = (b - 33) / 4 + 5, f = (b - 33) % 4;
+    return (uint64_t(5 + f) << (m - 2)) - 1;
+}
+
+template <int kMode>
+__global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, int skip_large)
+{
+    __shared__ uint32_t h[kNB];
+    for (int t = threadIdx.x; t < kNB; t += blockDim.x)
+        h[t] = 0;
+    __syncthreads();
     const uint64_t nthreads = uint64_t(gridDim.x) * blockDim.x;
     for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < d.n; i += nthreads) {
         uint64_t S, E;
         buffer_range<kMode>(d, i, S, E);
-        const uint64_t n = E - S;
-        if (skip_large && is_large(n))
+        if (skip_large && is_large(E - S))
             continue;
-        const uint32_t init = d.init ? d.init[i] : 0xFFFFFFFFu;
-        uint32_t R;
-        if (n < 4) {
+        atomicAdd(&h[bin_of(S, E)], 1u);
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < kNB; t += blockDim.x)
+        if (h[t])
+            atomicAdd(&so.bt->hist[t], h[t]);
+}
+
+__global__ __launch_bounds__(256) void k_bin_scan(Sorted so)
+{
+    __shared__ uint64_t s_start[kNB], s_count[kNB];
+    BinTable* bt = so.bt;
+    if (threadIdx.x == 0) {
+        uint64_t pos = 0, items = 0;
+        for (int b = 0; b < kNB; b++) {
+            const uint64_t c = bt->hist[b];
+            const uint64_t oct = (c + kG - 1) / kG;
+            bt->start[b] = pos;
+            bt->count[b] = c;
+            bt->cursor[b] = pos;
+            bt->items[b] = items;
+            bt->hist[b] = 0;
+            s_start[b] = pos;
+            s_count[b] = c;
+            pos += oct * kG;
+            if (b >= 2)   // bins 0-1 belong to k_entries_tiny
+                items += oct * (bin_kmax(b) + kOctetCost);
+        }
+        bt->items[kNB] = items;
+    }
+    __syncthreads();
+    // padding slots of each bin's last octet: empty
+    for (int t = threadIdx.x; t < kNB * kG; t += blockDim.x) {
+        const int b = t / kG, j = t % kG;
+        const uint64_t c = s_count[b];
+        const uint64_t slot = c + uint64_t(j);
+        if ((c % kG) && slot < (c + kG - 1) / kG * kG) {
+            so.desc[s_start[b] + slot] = u32x4{0u, 0u, 0u, 0u};
+            so.idx[s_start[b] + slot] = kNoIdx;
+        }
+    }
+}
+
+template <int kMode>
+__global__ __launch_bounds__(kThreads) void k_bin_scatter(BatchDesc d, Sorted so, int skip_large)
+{
+    __shared__ uint32_t cnt[kNB];
+    __shared__ uint64_t base[kNB];
+    for (int t = threadIdx.x; t < kNB; t += blockDim.x)
+        cnt[t] = 0;
+    __syncthreads();
+    for (uint64_t tile = uint64_t(blockIdx.x) * blockDim.x; tile < d.n;
+         tile += uint64_t(gridDim.x) * blockDim.x) {
+        const uint64_t i = tile + threadIdx.x;
+        int b = -1;
+        uint32_t lp = 0;
+        uint64_t S = 0, E = 0;
+        if (i < d.n) {
+            buffer_range<kMode>(d, i, S, E);
+            if (!(skip_large && is_large(E - S))) {
+                b = bin_of(S, E);
+                lp = atomicAdd(&cnt[b], 1u);
+            }
+        }
+        __syncthreads();
+        for (int t = threadIdx.x; t < kNB; t += blockDim.x)
+            if (cnt[t]) {
+                base[t] = atomicAdd(reinterpret_cast<unsigned long long*>(&so.bt->cursor[t]),
+                                    (unsigned long long)cnt[t]);
+                cnt[t] = 0;
+            }
+        __syncthreads();
+        if (b >= 0) {
+            const uint64_t pos = base[b] + lp;
+            so.desc[pos] = u32x4{uint32_t(S), uint32_t(S >> 32), uint32_t(E), uint32_t(E >> 32)};
+            so.idx[pos] = uint32_t(i);
+            if (d.init)
+                so.init[pos] = d.init[i];
+        }
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src)
+{
+    const uint32_t lo = __shfl(uint32_t(v), src, kWaveSize);
+    const uint32_t hi = __shfl(uint32_t(v >> 32), src, kWaveSize);
+    return (uint64_t(hi) << 32) | lo;
+}
+
+// Mask and init-inject the 16 bytes of lane piece `a` of entry [S, E): one
+// 64-bit clamp per piece, then 32-bit arithmetic per word.
+__device__ __forceinline__ int clamp32(int64_t x)
+{
+    return x < -32 ? -32 : (x > 32 ? 32 : int(x));
+}
+
+__device__ __forceinline__ uint32_t fix_word32(uint32_t w, int ds, int de, uint32_t init)
+{
+    const int lo = min(max(ds, 0), 4), hi = min(max(de, 0), 4);
+    const uint32_t mhi = uint32_t((1ull << (8 * hi)) - 1);
+    const uint32_t mlo = uint32_t((1ull << (8 * lo)) - 1);
+    w &= mhi & ~mlo;
+    const int dd = -ds;   // word address - S
+    const uint32_t inj =
+        uint32_t((uint64_t(init) << 24) >> (24 + 8 * min(max(dd, -3), 3)));
+    return w ^ ((dd > -4 && dd < 4) ? inj : 0u);
+}
+
+__device__ __forceinline__ u32x4 fix_piece(u32x4 w, uint64_t a, uint64_t S, uint64_t E,
+                                           uint32_t init)
+{
+    const int ds = clamp32(int64_t(S - a)), de = clamp32(int64_t(E - a));
+    w.x = fix_word32(w.x, ds, de, init);
+    w.y = fix_word32(w.y, ds - 4, de - 4, init);
+    w.z = fix_word32(w.z, ds - 8, de - 8, init);
+    w.w = fix_word32(w.w, ds - 12, de - 12, init);
+    return w;
+}
+
+// End of an entry: fold the slots, move to the entry end, XOR the group.
+// Every lane of the group returns the entry's raw state.
+__device__ __forceinline__ uint32_t entry_finish(const uint8_t* lds, int gl, uint32_t u0,
+                                                 uint32_t u1, uint32_t u2, uint32_t u3,
+                                                 uint64_t S, uint64_t E, uint64_t steps,
+                                                 uint32_t init)
+{
+    uint32_t R;
+    if (E - S >= 4) {
+        uint32_t y = plain_apply(lds, kX4Off, u0) ^ u1;
+        y = plain_apply(lds, kX4Off, y) ^ u2;
+        y = plain_apply(lds, kX4Off, y) ^ u3;
+        y = plain_apply(lds, kX4Off, y);
+        const uint64_t B = (S & ~uint64_t(15)) + steps * kStep;
+        const uint32_t pad = uint32_t(B - E);   // < 128
+        const uint32_t* cst = reinterpret_cast<const uint32_t*>(lds + kCstOff);
+        R = mulmod_dev(y, cst[gl * 128 + pad]);
+    } else {
+        // 0-3 bytes: byte steps from the initial state (lane 0 of the group)
+        R = 0;
+        if (gl == 0) {
             R = init;
-            const gu8* p = (const gu8*)S;
-            for (uint64_t b = 0; b < n; b++)
-                R = t0[(R ^ p[b]) & 0xFF] ^ (R >> 8);
-        } else {
+            const uint32_t* t0 = reinterpret_cast<const uint32_t*>(lds + kT0Off);
+            for (uint64_t a = S; a < E; a++)
+                R = t0[(R ^ *(const gu8*)a) & 0xFF] ^ (R >> 8);
+        }
+    }
+    R ^= __shfl_xor(R, 1, kWaveSize);
+    R ^= __shfl_xor(R, 2, kWaveSize);
+    R ^= __shfl_xor(R, 4, kWaveSize);
+    return R;
+}
+
+// Entries of at most one 128-byte window (bins 0-1; 100-byte log entries are
+// here): no Horner step and no per-entry multiply.  Byte b at distance m from
+// the entry end contributes X^m(b), read from a 129 x 256 LDS table, so a lane
+// does 16 lookups for its 16 bytes and the group XORs its 8 lanes.  Eight
+// octets (64 entries, one descriptor per lane) share one load round.
+__global__ __launch_bounds__(kThreads, 1) void k_entries_tiny(BatchDesc d, Sorted so)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsTiny];
+    fill_plain(lds, 0, &g_tab.pos[0][0], 129 * 256);
+    __syncthreads();
+    const uint32_t* tab = reinterpret_cast<const uint32_t*>(lds);
+
+    const int lane = threadIdx.x & (kWaveSize - 1);
+    const int g = lane >> 3, gl = lane & 7;
+    const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerGroup +
+                          __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
+    const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerGroup;
+    const uint64_t s0 = so.bt->start[0], s1 = so.bt->start[2];
+    const uint64_t rounds = (s1 - s0 + 63) / 64;
+    const bool finalize = d.flags & RAMCRC_FINALIZE;
+    const uint64_t dummy = reinterpret_cast<uint64_t>(so.bt);
+
+    for (uint64_t r = wave; r < rounds; r += nwaves) {
+        const uint64_t slot = s0 + r * 64 + lane;
+        u32x4 dd = {0u, 0u, 0u, 0u};
+        uint32_t didx = kNoIdx, dinit = 0xFFFFFFFFu;
+        if (slot < s1) {
+            dd = so.desc[slot];
+            didx = so.idx[slot];
+            if (d.init)
+                dinit = so.init[slot];
+        }
+        const uint64_t dS = (uint64_t(dd.y) << 32) | dd.x;
+        const uint64_t dE = (uint64_t(dd.w) << 32) | dd.z;
+        u32x4 w[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const uint64_t S = shfl64(dS, q * kG + g), E = shfl64(dE, q * kG + g);
             const uint64_t A = S & ~uint64_t(15);
-            const uint64_t B = (E + 15) & ~uint64_t(15);
+            const uint64_t a = A + gl * 16;
+            const bool big = E - S >= 4;
+            const bool ok = big && a < E;
+            const u32x4 v = load16(ok ? a : (big ? A : dummy));
+            w[q] = ok ? v : u32x4{0u, 0u, 0u, 0u};
+        }
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int src = q * kG + g;
+            const uint64_t S = shfl64(dS, src), E = shfl64(dE, src);
+            const uint32_t init = __shfl(dinit, src, kWaveSize);
+            const uint64_t a = (S & ~uint64_t(15)) + gl * 16;
+            uint32_t R = 0;
+            if (E - S >= 4) {
+                const u32x4 x = fix_piece(w[q], a, S, E, init);
+                // table row m = distance of the byte from E; bytes at or past E
+                // are zero and clamp to row 128 (X^128(0) = 0)
+                const uint32_t e10 = uint32_t(E - a) << 10;
+                const uint32_t ws[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+#pragma unroll
+                    for (int t = 0; t < 4; t++) {
+                        const uint32_t c = uint32_t(4 * j + t) << 10;
+                        const uint32_t row = min(e10 - c, 128u << 10);
+                        const uint32_t byte = (ws[j] >> (8 * t)) & 0xFF;
+                        R ^= tab[(row | (byte << 2)) >> 2];
+                    }
+            } else if (gl == 0) {
+                R = init;
+                for (uint64_t p = S; p < E; p++)
+                    R = tab[256 + ((R ^ *(const gu8*)p) & 0xFF)] ^ (R >> 8);
+            }
+            R ^= __shfl_xor(R, 1, kWaveSize);
+            R ^= __shfl_xor(R, 2, kWaveSize);
+            R ^= __shfl_xor(R, 4, kWaveSize);
+            const uint32_t ix = __shfl(didx, src, kWaveSize);
+            if (gl == 0 && ix != kNoIdx)
+                d.out[ix] = finalize ? ~R : R;
+        }
+    }
+}
+
+// Entries of two or more 128-byte steps (bins >= 2).  One octet (8 entries,
+// one per lane group) at a time, kPU-deep ping-pong prefetch of the steps, the
+// next octet's descriptor prefetched during the current one.  Waves split the
+// bins by estimated work (steps + kOctetCost per octet).
+__global__ __launch_bounds__(kThreads, 1) void k_entries(BatchDesc d, Sorted so)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsEntries];
+    fill_replicated(lds, g_tab.stride_small);
+    fill_plain(lds, kX4Off, &g_tab.comb[0].t[0][0], 1024);
+    fill_plain(lds, kCstOff, &g_tab.ecst[0][0], 1024);
+    fill_plain(lds, kT0Off, g_tab.t0.t, 256);
+    uint64_t* s_items = reinterpret_cast<uint64_t*>(lds + kBinOff);   // kNB + 1
+    uint64_t* s_start = s_items + (kNB + 1);                          // kNB
+    for (int t = threadIdx.x; t <= kNB; t += blockDim.x) {
+        s_items[t] = so.bt->items[t];
+        if (t < kNB)
+            s_start[t] = so.bt->start[t];
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & (kWaveSize - 1);
+    const int g = lane >> 3, gl = lane & 7;
+    const RepOp op(lane);
+    const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerGroup +
+                          __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
+    const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerGroup;
+    const uint64_t T = s_items[kNB];
+    const uint64_t lo = T * wave / nwaves, hi = T * (wave + 1) / nwaves;
+    const bool finalize = d.flags & RAMCRC_FINALIZE;
+    const uint64_t dummy = reinterpret_cast<uint64_t>(so.bt);   // device memory, 16 B aligned
+
+    for (int b = 2; b < kNB; b++) {
+        const uint64_t ib = s_items[b], ie = s_items[b + 1];
+        if (ie <= lo || ib == ie)
+            continue;
+        if (ib >= hi)
+            break;
+        const uint64_t cost = bin_kmax(b) + kOctetCost;
+        const uint64_t oa = ((lo > ib ? lo : ib) - ib + cost - 1) / cost;
+        const uint64_t ob = ((hi < ie ? hi : ie) - ib + cost - 1) / cost;
+        const uint64_t sb = s_start[b];
+        if (oa >= ob)
+            continue;
+        u32x4 nd = so.desc[sb + oa * kG + g];
+        uint32_t nix = so.idx[sb + oa * kG + g];
+        uint32_t ninit = d.init ? so.init[sb + oa * kG + g] : 0xFFFFFFFFu;
+        for (uint64_t o = oa; o < ob; o++) {
+            const u32x4 dd = nd;
+            const uint32_t ix = nix, init = ninit;
+            if (o + 1 < ob) {   // prefetch the next octet's descriptor
+                const uint64_t ns = sb + (o + 1) * kG + g;
+                nd = so.desc[ns];
+                nix = so.idx[ns];
+                if (d.init)
+                    ninit = so.init[ns];
+            }
+            const uint64_t S = (uint64_t(dd.y) << 32) | dd.x;
+            const uint64_t E = (uint64_t(dd.w) << 32) | dd.z;
+            const uint64_t steps = (ix != kNoIdx && E - S >= 4) ? entry_steps(S, E) : 0;
+            const uint64_t A = S & ~uint64_t(15);
+            const uint64_t p0 = A + gl * 16;
+            // longest / shortest entry of the octet (padding slots excluded)
+            uint32_t kmax32 = uint32_t(steps), kmin32 = steps ? uint32_t(steps) : 0xFFFFFFFFu;
+#pragma unroll
+            for (int s = 8; s < 64; s <<= 1) {
+                kmax32 = max(kmax32, uint32_t(__shfl_xor(kmax32, s, kWaveSize)));
+                kmin32 = min(kmin32, uint32_t(__shfl_xor(kmin32, s, kWaveSize)));
+            }
+            const uint64_t Koct = __builtin_amdgcn_readfirstlane(kmax32);
+            const uint64_t Kmin = __builtin_amdgcn_readfirstlane(kmin32);
+            const uint64_t safe = steps ? A : dummy;   // steps == 0: padding slot
+            auto ldk = [&](uint64_t k) -> u32x4 {
+                const uint64_t a = p0 + k * kStep;
+                const bool ok = k < steps && a < E && a + 16 > S;
+                const u32x4 v = load16(ok ? a : safe);
+                return ok ? v : u32x4{0u, 0u, 0u, 0u};
+            };
             uint32_t u0 = 0, u1 = 0, u2 = 0, u3 = 0;
-            for (uint64_t a = A; a < B; a += 16) {
-                u32x4 w = load16(a);
-                if (a < S + 4 || a + 16 > E) {
-                    w.x = fix_word(w.x, a + 0, S, E, init);
-                    w.y = fix_word(w.y, a + 4, S, E, init);
-                    w.z = fix_word(w.z, a + 8, S, E, init);
-                    w.w = fix_word(w.w, a + 12, S, E, init);
-                }
+            auto stepk = [&](u32x4 w, uint64_t k) {
+                w = fix_piece(w, p0 + k * kStep, S, E, init);
+                const bool live = k < steps;
+                const uint32_t v0 = op.apply(lds, u0, w.x), v1 = op.apply(lds, u1, w.y);
+                const uint32_t v2 = op.apply(lds, u2, w.z), v3 = op.apply(lds, u3, w.w);
+                u0 = live ? v0 : u0;
+                u1 = live ? v1 : u1;
+                u2 = live ? v2 : u2;
+                u3 = live ? v3 : u3;
+            };
+            // Steps 1 .. Kmin-2 are interior for every live group: no masks,
+            // no init, unconditional loads (padding groups read their safe word
+            // and their accumulators are never stored).
+            const gu32x4* pb = gptr16(steps ? p0 : dummy);
+            const uint64_t bstride = steps ? kStep / 16 : 0;
+            auto ldf = [&](uint64_t k) -> u32x4 { return __builtin_nontemporal_load(pb + k * bstride); };
+            auto stepf = [&](const u32x4& w) {
                 u0 = op.apply(lds, u0, w.x);
                 u1 = op.apply(lds, u1, w.y);
                 u2 = op.apply(lds, u2, w.z);
                 u3 = op.apply(lds, u3, w.w);
+            };
+            if (Kmin != 0xFFFFFFFFull && Kmin >= 3 && Koct - Kmin <= 1) {
+                const uint64_t kb = Kmin - 1;          // body = [1, kb)
+                const u32x4 wh = ldk(0);
+                const u32x4 wt0 = ldk(kb);
+                const u32x4 wt1 = ldk(kb + 1 < Koct ? kb + 1 : kb);
+                u32x4 Abuf[kPU], Bbuf[kPU];
+#pragma unroll
+                for (int j = 0; j < kPU; j++)
+                    Abuf[j] = ldf(1 + j < kb ? 1 + j : kb - 1);
+                stepk(wh, 0);
+                uint64_t k = 1;
+                for (; k + 2 * kPU <= kb; k += 2 * kPU) {
+#pragma unroll
+                    for (int j = 0; j < kPU; j++)
+                        Bbuf[j] = ldf(k + kPU + j);
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int j = 0; j < kPU; j++)
+                        stepf(Abuf[j]);
+#pragma unroll
+                    for (int j = 0; j < kPU; j++)
+                        Abuf[j] = ldf(k + 2 * kPU + j < kb ? k + 2 * kPU + j : kb - 1);
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int j = 0; j < kPU; j++)
+                        stepf(Bbuf[j]);
+                }
+#pragma unroll
+                for (int j = 0; j < kPU; j++)
+                    if (k + j < kb)
+                        stepf(Abuf[j]);
+                if (k + kPU < kb) {
+#pragma unroll
+                    for (int j = 0; j < kPU; j++)
+                        Bbuf[j] = ldf(k + kPU + j < kb ? k + kPU + j : kb - 1);
+#pragma unroll
+                    for (int j = 0; j < kPU; j++)
+                        if (k + kPU + j < kb)
+                            stepf(Bbuf[j]);
+                }
+                stepk(wt0, kb);
+                if (kb + 1 < Koct)
+                    stepk(wt1, kb + 1);
+            } else {
+                // ragged octet (log-scale bins): every step checked
+                u32x4 Abuf[kPU], Bbuf[kPU];
+#pragma unroll
+                for (int j = 0; j < kPU; j++)
+                    Abuf[j] = ldk(j);
+                uint64_t k = 0;
+                for (; k + 2 * kPU <= Koct; k += 2 * kPU) {
+#pragma unroll
+                    for (int j = 0; j < kPU; j++)
+                        Bbuf[j] = ldk(k + kPU + j);
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int j = 0; j < kPU; j++)
+                        stepk(Abuf[j], k + j);
+#pragma unroll
+                    for (int j = 0; j < kPU; j++)
+                        Abuf[j] = ldk(k + 2 * kPU + j);
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int j = 0; j < kPU; j++)
+                        stepk(Bbuf[j], k + kPU + j);
+                }
+#pragma unroll
+                for (int j = 0; j < kPU; j++)
+                    if (k + j < Koct)
+                        stepk(Abuf[j], k + j);
+                if (k + kPU < Koct) {
+#pragma unroll
+                    for (int j = 0; j < kPU; j++)
+                        Bbuf[j] = ldk(k + kPU + j);
+#pragma unroll
+                    for (int j = 0; j < kPU; j++)
+                        if (k + kPU + j < Koct)
+                            stepk(Bbuf[j], k + kPU + j);
+                }
             }
-            uint32_t y = plain_apply(lds, kX4Off, u0) ^ u1;
-            y = plain_apply(lds, kX4Off, y) ^ u2;
-            y = plain_apply(lds, kX4Off, y) ^ u3;
-            y = plain_apply(lds, kX4Off, y);
-            const uint32_t pad = uint32_t(B - E);
-            R = pad ? mulmod_dev(y, g_tab.xinv[pad]) : y;
+            const uint32_t R = entry_finish(lds, gl, u0, u1, u2, u3, S, E, steps, init);
+            if (gl == 0 && ix != kNoIdx)
+                d.out[ix] = finalize ? ~R : R;
         }
-        d.out[i] = (d.flags & RAMCRC_FINALIZE) ? ~R : R;
     }
 }
 
@@ -668,6 +1126,12 @@ struct ramcrc_ctx {
     uint64_t* group_pref = nullptr;
     uint64_t group_cap = 0;
     uint32_t* status = nullptr;
+    // small-entry binning
+    BinTable* bins = nullptr;
+    u32x4* sdesc = nullptr;
+    uint32_t* sidx = nullptr;
+    uint32_t* sinit = nullptr;
+    uint64_t sorted_cap = 0;
     // host staging for ramcrc_batch_host / ramcrc_stream_host
     uint8_t* h_stage = nullptr;
     uint64_t h_stage_cap = 0;
@@ -772,6 +1236,55 @@ struct ScanTimer {
     }
 };
 
+int reserve_sorted(ramcrc_ctx* c, uint64_t n)
+{
+    const uint64_t need = n + uint64_t(kG) * kNB;
+    if (c->sorted_cap >= need)
+        return RAMCRC_OK;
+    uint64_t cap = c->sorted_cap;
+    int rc = grow_device(reinterpret_cast<void**>(&c->sdesc), &cap, need, sizeof(u32x4));
+    if (rc)
+        return rc;
+    cap = c->sorted_cap;
+    rc = grow_device(reinterpret_cast<void**>(&c->sidx), &cap, need, sizeof(uint32_t));
+    if (rc)
+        return rc;
+    cap = c->sorted_cap;
+    rc = grow_device(reinterpret_cast<void**>(&c->sinit), &cap, need, sizeof(uint32_t));
+    if (rc)
+        return rc;
+    c->sorted_cap = cap;
+    return RAMCRC_OK;
+}
+
+// Small-entry path: bin by step count, scatter into bin order, scan.
+template <int kMode>
+int launch_binned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_large)
+{
+    if (d.n >= (1ull << 32))
+        return RAMCRC_EINVAL;   // sorted slots keep 32-bit entry indices
+    int rc = reserve_sorted(c, d.n);
+    if (rc)
+        return rc;
+    Sorted so{c->bins, c->sdesc, c->sidx, c->sinit};
+    uint64_t grid = (d.n + kThreads - 1) / kThreads;
+    if (grid > uint64_t(4 * c->ncu))
+        grid = 4 * c->ncu;
+    hipLaunchKernelGGL(k_bin_count<kMode>, dim3(grid), dim3(kThreads), 0, s, d, so, skip_large);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(256), 0, s, so);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_bin_scatter<kMode>, dim3(grid), dim3(kThreads), 0, s, d, so, skip_large);
+    HIPCHK(hipGetLastError());
+    {
+        ScanTimer t(c, s);
+        hipLaunchKernelGGL(k_entries_tiny, dim3(c->ncu), dim3(kThreads), 0, s, d, so);
+        hipLaunchKernelGGL(k_entries, dim3(c->ncu), dim3(kThreads), 0, s, d, so);
+    }
+    HIPCHK(hipGetLastError());
+    return RAMCRC_OK;
+}
+
 template <int kMode>
 int launch_planned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s)
 {
@@ -788,9 +1301,7 @@ int launch_planned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s)
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_combine<kMode>, dim3((d.n + 3) / 4), dim3(256), 0, s, d, pl, uint64_t(0));
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_entries<kMode>, dim3(c->ncu), dim3(kThreads), 0, s, d, 1);
-    HIPCHK(hipGetLastError());
-    return RAMCRC_OK;
+    return launch_binned<kMode>(c, d, s, 1);
 }
 
 }  // namespace
@@ -854,6 +1365,11 @@ int ramcrc_ctx_create(int device, ramcrc_ctx** out)
         return RAMCRC_ENOMEM;
     }
     (void)hipMemset(c->status, 0, 16);
+    if (hipMalloc(reinterpret_cast<void**>(&c->bins), sizeof(BinTable)) != hipSuccess) {
+        ramcrc_ctx_destroy(c);
+        return RAMCRC_ENOMEM;
+    }
+    (void)hipMemset(c->bins, 0, sizeof(BinTable));   // hist must start at zero
     *out = c;
     return RAMCRC_OK;
 }
@@ -868,6 +1384,10 @@ int ramcrc_ctx_destroy(ramcrc_ctx* c)
     if (c->plan_local) (void)hipFree(c->plan_local);
     if (c->group_pref) (void)hipFree(c->group_pref);
     if (c->status) (void)hipFree(c->status);
+    if (c->bins) (void)hipFree(c->bins);
+    if (c->sdesc) (void)hipFree(c->sdesc);
+    if (c->sidx) (void)hipFree(c->sidx);
+    if (c->sinit) (void)hipFree(c->sinit);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -953,12 +1473,7 @@ int ramcrc_segments_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_bytes
     d.out = d_out;
     d.flags = flags;
     if (seg_bytes < kLargeMin) {
-        {
-            ScanTimer t(c, s);
-            hipLaunchKernelGGL(k_entries<kSegUniform>, dim3(c->ncu), dim3(kThreads), 0, s, d, 0);
-        }
-        HIPCHK(hipGetLastError());
-        return RAMCRC_OK;
+        return launch_binned<kSegUniform>(c, d, s, 0);
     }
     const uint64_t B = reinterpret_cast<uint64_t>(d_base);
     if ((B % kChunk) == 0 && (seg_bytes % kChunk) == 0) {
@@ -1028,12 +1543,7 @@ int ramcrc_entries_device(ramcrc_ctx* c, const void* d_base, const uint64_t* d_o
     d.init = d_init;
     d.out = d_out;
     d.flags = flags;
-    {
-        ScanTimer t(c, s);
-        hipLaunchKernelGGL(k_entries<kTable>, dim3(c->ncu), dim3(kThreads), 0, s, d, 0);
-    }
-    HIPCHK(hipGetLastError());
-    return RAMCRC_OK;
+    return launch_binned<kTable>(c, d, s, 0);
 }
 
 int ramcrc_batch_host(ramcrc_ctx* c, const void* const* ptrs, const uint64_t* lens,
