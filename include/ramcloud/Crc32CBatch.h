@@ -1,0 +1,132 @@
+/* Opt-in batch CRC32C on an MI355X for RAMCloud callers that hold many
+ * independent buffers at once:
+ *
+ *   - the backup recovery scan: every loaded replica frame is a contiguous
+ *     8 MiB buffer (BackupStorage::Frame::load, src/BackupStorage.h:227)
+ *     verified independently in BackupMasterRecovery::CyclicReplicaBuffer::
+ *     buildNext (src/BackupMasterRecovery.cc:743-809);
+ *   - the recovery-master replay: one Object::computeChecksum per object of a
+ *     recovery segment (src/ObjectManager.cc:659-663, src/Object.cc:805-819).
+ *
+ * Each call returns exactly what `Crc32C c; c.update(buf_i, len_i);
+ * c.getResult()` returns for every buffer (or the raw running value, for
+ * chaining), computed by libramcrc's gfx950 kernels.  Comparison against the
+ * stored checksums stays with the caller, as in the reference
+ * (src/Segment.cc:793-797, src/ObjectManager.cc:664-669).
+ *
+ * Errors from the C ABI (include/ramcrc.h) become RAMCRC_BATCH_THROW(msg),
+ * which is `throw FatalError(HERE, msg)` inside RAMCloud (src/Exception.h:70)
+ * and std::runtime_error elsewhere.  No HIP header is needed by callers.
+ */
+#ifndef RAMCLOUD_CRC32CBATCH_H
+#define RAMCLOUD_CRC32CBATCH_H
+
+#include <stdint.h>
+
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "ramcrc.h"
+
+#ifndef RAMCRC_BATCH_THROW
+#if defined(RAMCLOUD_EXCEPTION_H)
+#define RAMCRC_BATCH_THROW(msg) throw RAMCloud::FatalError(HERE, msg)
+#else
+#include <stdexcept>
+#define RAMCRC_BATCH_THROW(msg) throw std::runtime_error(msg)
+#endif
+#endif
+
+namespace RAMCloud {
+
+class Crc32CBatch {
+  public:
+    /// Binds to a GPU lazily on first use (never at static-init time).
+    explicit Crc32CBatch(int device = 0)
+        : device(device)
+        , ctx(NULL)
+    {
+    }
+
+    ~Crc32CBatch()
+    {
+        if (ctx)
+            ramcrc_ctx_destroy(ctx);
+    }
+
+    /**
+     * CRC32C of host buffers (e.g. loaded replica frames): staged through
+     * pinned memory to the GPU and back.  Synchronous.
+     * \param buffers
+     *      (pointer, length) of every buffer.
+     * \param finalize
+     *      true: getResult() values; false: raw running values.
+     */
+    std::vector<uint32_t>
+    hostBuffers(const std::vector<std::pair<const void*, uint64_t> >& buffers,
+                bool finalize = true)
+    {
+        std::vector<const void*> ptrs;
+        std::vector<uint64_t> lens;
+        for (size_t i = 0; i < buffers.size(); i++) {
+            ptrs.push_back(buffers[i].first);
+            lens.push_back(buffers[i].second);
+        }
+        std::vector<uint32_t> out(buffers.size());
+        if (!buffers.empty())
+            check(ramcrc_batch_host(context(), &ptrs[0], &lens[0], NULL, &out[0],
+                                    out.size(), finalize ? RAMCRC_FINALIZE : 0u),
+                  "ramcrc_batch_host");
+        return out;
+    }
+
+    /// Device-resident uniform segments (the recovery-scan shard): d_out[i]
+    /// for segment i = d_base + i * segmentBytes.  Asynchronous on `stream`.
+    void
+    deviceSegments(const void* d_base, uint64_t segmentBytes, uint64_t count,
+                   uint32_t* d_out, void* stream = NULL, bool finalize = true)
+    {
+        check(ramcrc_segments_device(context(), d_base, segmentBytes, count, NULL, d_out,
+                                     finalize ? RAMCRC_FINALIZE : 0u, stream),
+              "ramcrc_segments_device");
+    }
+
+    /// Device-resident (offset, length) table, e.g. the (off + 4, len - 4)
+    /// object ranges of a recovery segment.  Asynchronous on `stream`.
+    void
+    deviceBatch(const void* d_base, const uint64_t* d_off, const uint64_t* d_len,
+                const uint32_t* d_init, uint32_t* d_out, uint64_t count, void* stream = NULL,
+                bool finalize = true)
+    {
+        check(ramcrc_batch_device(context(), d_base, d_off, d_len, d_init, d_out, count,
+                                  finalize ? RAMCRC_FINALIZE : 0u, stream),
+              "ramcrc_batch_device");
+    }
+
+  private:
+    ramcrc_ctx*
+    context()
+    {
+        if (!ctx)
+            check(ramcrc_ctx_create(device, &ctx), "ramcrc_ctx_create");
+        return ctx;
+    }
+
+    static void
+    check(int rc, const char* what)
+    {
+        if (rc != RAMCRC_OK)
+            RAMCRC_BATCH_THROW(std::string(what) + ": " + ramcrc_strerror(rc));
+    }
+
+    int device;
+    ramcrc_ctx* ctx;
+
+    Crc32CBatch(const Crc32CBatch&);             // not copyable
+    Crc32CBatch& operator=(const Crc32CBatch&);
+};
+
+} // namespace RAMCloud
+
+#endif // RAMCLOUD_CRC32CBATCH_H

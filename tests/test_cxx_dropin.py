@@ -3,6 +3,8 @@ used exactly as RAMCloud's callers and src/Crc32CTest.cc use the reference class
 import os
 import subprocess
 
+import pytest
+
 from conftest import ROOT
 
 
@@ -28,3 +30,37 @@ def test_cxx_dropin(golden, ramcrc, tmp_path):
     out = subprocess.run([str(exe), str(vec)], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "failures=0" in out.stdout
+
+
+def _build_batch_test(ramcrc, tmp_path):
+    exe = tmp_path / "batch_test"
+    libdir = os.path.dirname(ramcrc.lib_path())
+    subprocess.check_call([
+        "g++", "-std=c++11", "-O2", "-Wall", "-Werror",
+        "-I" + os.path.join(ROOT, "tests", "cpp"),
+        "-I" + os.path.join(ROOT, "include", "ramcloud"),
+        "-I" + os.path.join(ROOT, "include"),
+        os.path.join(ROOT, "tests", "cpp", "batch_test.cc"),
+        os.path.join(ROOT, "ramcloud_amd", "dropin", "Crc32C.cc"),
+        "-L" + libdir, "-lramcrc", "-Wl,-rpath," + libdir, "-o", str(exe)])
+    return exe
+
+
+def test_cxx_batch_wrapper_without_gpu(ramcrc, tmp_path):
+    """Crc32CBatch compiles against the C ABI alone and reports a missing GPU
+    as an exception (never a crash); skipped where a GPU is visible."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by test_cxx_batch_wrapper_gpu")
+    exe = _build_batch_test(ramcrc, tmp_path)
+    out = subprocess.run([str(exe), "nodev"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "exception" in out.stdout
+
+
+@pytest.mark.gpu
+def test_cxx_batch_wrapper_gpu(ramcrc, tmp_path):
+    exe = _build_batch_test(ramcrc, tmp_path)
+    out = subprocess.run([str(exe), "gpu"], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "0 mismatches" in out.stdout
