@@ -39,22 +39,50 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=False):
-    if not force and not _stale():
-        return LIB
-    os.makedirs(LIBDIR, exist_ok=True)
-    tmp = LIB + ".tmp"
+def _compile(out, defines=(), verbose=False):
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    tmp = out + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-fconstexpr-steps=1000000000", "-Wall", "-Wno-unused-function",
            "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
+    cmd += ["-D" + d for d in defines]
     cmd += [os.path.join(CSRC, s) for s in SOURCES]
     cmd += ["-o", tmp]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, out)
+    return out
+
+
+def build(force=False, verbose=False):
+    if not force and not _stale():
+        return LIB
+    return _compile(LIB, verbose=verbose)
+
+
+# Tuning variants (A/B on the GPU box: RAMCRC_LIB=<path> python bench.py ...)
+VARIANTS = {
+    "u4_c18": ["RAMCRC_UNROLL=4", "RAMCRC_CHUNK_SHIFT=18"],
+    "u2_c18": ["RAMCRC_UNROLL=2", "RAMCRC_CHUNK_SHIFT=18"],
+    "u6_c18": ["RAMCRC_UNROLL=6", "RAMCRC_CHUNK_SHIFT=18"],
+    "u4_c19": ["RAMCRC_UNROLL=4", "RAMCRC_CHUNK_SHIFT=19"],
+    "u4_c17": ["RAMCRC_UNROLL=4", "RAMCRC_CHUNK_SHIFT=17"],
+    "u4_c20": ["RAMCRC_UNROLL=4", "RAMCRC_CHUNK_SHIFT=20"],
+}
+
+
+def build_variants(names=None, verbose=False):
+    from concurrent.futures import ThreadPoolExecutor
+    names = names or list(VARIANTS)
+    outs = {n: os.path.join(LIBDIR, "variants", f"libramcrc_{n}.so") for n in names}
+    with ThreadPoolExecutor(max_workers=4) as ex:
+        list(ex.map(lambda n: _compile(outs[n], VARIANTS[n], verbose), names))
+    return outs
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    if "--variants" in sys.argv:
+        print(build_variants(verbose=True))
+    else:
+        print(build(force="--force" in sys.argv, verbose=True))

@@ -58,10 +58,23 @@ constexpr int kWaveSize = 64;
 constexpr int kWavesPerGroup = 16;                 // 1024-thread workgroups, 1 per CU
 constexpr int kThreads = kWaveSize * kWavesPerGroup;
 constexpr uint32_t kBlock = 1024;                  // bytes per wave step
-constexpr int kChunkShift = 18;
+#ifndef RAMCRC_CHUNK_SHIFT
+#define RAMCRC_CHUNK_SHIFT 18
+#endif
+#ifndef RAMCRC_UNROLL
+#define RAMCRC_UNROLL 4
+#endif
+#ifndef RAMCRC_ASM_XOR3
+#define RAMCRC_ASM_XOR3 1
+#endif
+#ifndef RAMCRC_DYNAMIC
+#define RAMCRC_DYNAMIC 0
+#endif
+constexpr int kChunkShift = RAMCRC_CHUNK_SHIFT;
 constexpr uint64_t kChunk = 1ull << kChunkShift;   // 256 KiB per wave work item
 constexpr uint64_t kLargeMin = 64 * 1024;          // batch API threshold
-constexpr int kUnroll = 8;                         // blocks in flight per wave
+constexpr int kUnroll = RAMCRC_UNROLL;             // blocks per register group (x2 in flight)
+constexpr bool kDynamic = RAMCRC_DYNAMIC;          // waves dequeue chunks from a counter
 
 // ------------------------------------------------------------------ tables
 struct DeviceTables {
@@ -155,6 +168,17 @@ __device__ __forceinline__ void fill_plain(uint8_t* lds, uint32_t off, const uin
         dst[i] = src[i];
 }
 
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+#if RAMCRC_ASM_XOR3
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+#else
+    return a ^ b ^ c;
+#endif
+}
+
 // Per-lane constant for table k: [byte0 = bank offset (+128 for odd k),
 // byte2 = region].
 __device__ __forceinline__ uint32_t lane_reg(int k, int lane)
@@ -178,14 +202,16 @@ struct RepOp {
           lr3(lane_reg(3, lane))
     {
     }
-    // X^stride(u) ^ w through the replicated tables.
+    // X^stride(u) ^ w through the replicated tables.  The four lookups are
+    // consumed by two 3-input XORs, v_bitop3_b32 0x96 (inline asm so that hipcc waits once for all
+    // four LDS reads instead of chaining 2-input XORs behind one wait each).
     __device__ __forceinline__ uint32_t apply(const uint8_t* lds, uint32_t u, uint32_t w) const
     {
         const uint32_t a = *reinterpret_cast<const uint32_t*>(lds + rep_addr<0>(u, lr0));
         const uint32_t b = *reinterpret_cast<const uint32_t*>(lds + rep_addr<1>(u, lr1));
         const uint32_t c = *reinterpret_cast<const uint32_t*>(lds + rep_addr<2>(u, lr2));
         const uint32_t d = *reinterpret_cast<const uint32_t*>(lds + rep_addr<3>(u, lr3));
-        return (a ^ b ^ w) ^ (c ^ d);
+        return xor3(xor3(a, b, w), c, d);
     }
 };
 
@@ -263,6 +289,7 @@ struct BatchDesc {
     const uint32_t* init;    // nullable
     uint32_t* out;
     uint32_t flags;
+    uint32_t cshift;         // log2 chunk bytes of this launch (k_chunks/k_combine)
 };
 
 // Buffer addressing modes.
@@ -285,9 +312,9 @@ __device__ __forceinline__ void buffer_range(const BatchDesc& d, uint64_t i, uin
     }
 }
 
-__device__ __forceinline__ uint64_t chunk_count(uint64_t S, uint64_t E)
+__device__ __forceinline__ uint64_t chunk_count(uint64_t S, uint64_t E, uint32_t cshift)
 {
-    return ((E - 1) >> kChunkShift) - (S >> kChunkShift) + 1;
+    return ((E - 1) >> cshift) - (S >> cshift) + 1;
 }
 
 struct Plan {
@@ -297,6 +324,7 @@ struct Plan {
     uint32_t* partials;
     uint64_t partials_cap;
     uint32_t* status;      // bit 0: partials overflow
+    unsigned long long* ticket;   // chunk dequeue counter; zero between launches
 };
 
 __device__ __forceinline__ bool is_large(uint64_t len) { return len >= kLargeMin; }
@@ -458,7 +486,19 @@ __global__ __launch_bounds__(kThreads, 1) void k_chunks(BatchDesc d, Plan pl, ui
             atomicOr(pl.status, 1u);
         return;
     }
-    for (uint64_t g = wave; g < total; g += nwaves) {
+    // Work: chunk g -> (buffer i, chunk k).  Dynamic: lane 0 takes tickets
+    // from a device counter (one ahead, so the atomic's latency hides behind
+    // a chunk); static: grid stride.
+    auto take = [&]() -> uint64_t {
+        uint64_t t = 0;
+        if (lane == 0)
+            t = atomicAdd(pl.ticket, 1ull);
+        return __builtin_amdgcn_readfirstlane(uint32_t(t)) |
+               (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(t >> 32))) << 32);
+    };
+    uint64_t g = kDynamic ? take() : wave;
+    while (g < total) {
+        const uint64_t gnext = kDynamic ? take() : g + nwaves;
         uint64_t i, k;
         if (kMode == kSegAligned) {
             i = g / per_seg;
@@ -469,14 +509,15 @@ __global__ __launch_bounds__(kThreads, 1) void k_chunks(BatchDesc d, Plan pl, ui
         uint64_t S, E;
         buffer_range<kMode>(d, i, S, E);
         const uint32_t init = d.init ? d.init[i] : 0xFFFFFFFFu;
-        const uint64_t cs = S >> kChunkShift;
-        const uint64_t c_lo = (cs + k) << kChunkShift;
+        const uint64_t cs = S >> d.cshift;
+        const uint64_t c_lo = (cs + k) << d.cshift;
         const uint64_t lo = c_lo > S ? c_lo : S;
-        const uint64_t c_hi = c_lo + kChunk;
+        const uint64_t c_hi = c_lo + (1ull << d.cshift);
         const uint64_t hi = c_hi < E ? c_hi : E;
         const uint32_t r = scan_chunk(lds, op, lane, S, E, init, lo, hi);
         if (lane == 0)
             pl.partials[g] = r;
+        g = gnext;
     }
 }
 
@@ -486,6 +527,8 @@ __global__ __launch_bounds__(256) void k_combine(BatchDesc d, Plan pl, uint64_t 
 {
     const int lane = threadIdx.x & (kWaveSize - 1);
     const uint64_t i = uint64_t(blockIdx.x) * (256 / kWaveSize) + threadIdx.x / kWaveSize;
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        *pl.ticket = 0;   // k_chunks of this launch is complete (same stream)
     if (i >= d.n)
         return;
     uint64_t S, E;
@@ -496,13 +539,13 @@ __global__ __launch_bounds__(256) void k_combine(BatchDesc d, Plan pl, uint64_t 
         return;   // k_chunks refused the launch (partials overflow)
     const uint64_t g0 = kMode == kSegAligned ? i * per_seg
                                              : pl.group_pref[i / kThreads] + pl.local[i];
-    const uint64_t cnt = chunk_count(S, E);
-    const uint64_t cs = S >> kChunkShift;
+    const uint64_t cnt = chunk_count(S, E, d.cshift);
+    const uint64_t cs = S >> d.cshift;
     const uint64_t pend = (E + kBlock - 1) & ~uint64_t(kBlock - 1);
     uint32_t R = 0;
     for (uint64_t k = lane; k < cnt; k += kWaveSize) {
         const uint32_t r = pl.partials[g0 + k];
-        const uint64_t ek = (k + 1 == cnt) ? pend : ((cs + k + 1) << kChunkShift);
+        const uint64_t ek = (k + 1 == cnt) ? pend : ((cs + k + 1) << d.cshift);
         const uint64_t t = (pend - ek) / kBlock;
         R ^= t ? mulmod_dev(r, xpow_blocks(t)) : r;
     }
@@ -532,7 +575,6 @@ __global__ __launch_bounds__(256) void k_combine(BatchDesc d, Plan pl, uint64_t 
 constexpr int kG = 8;                      // lanes per entry group
 constexpr uint64_t kStep = kG * 16;        // bytes per group step
 constexpr int kNB = 161;                   // step-count bins
-constexpr int kEU = 8;                     // steps per load round (batched bins)
 constexpr int kPU = 4;                     // ping-pong depth (pipelined bins)
 constexpr uint32_t kNoIdx = 0xFFFFFFFFu;   // empty slot
 constexpr uint64_t kOctetCost = 3;         // per-octet overhead in step units (work split)
@@ -1024,7 +1066,7 @@ __global__ __launch_bounds__(kThreads) void k_plan_count(BatchDesc d, Plan pl)
     if (i < d.n) {
         uint64_t S, E;
         buffer_range<kMode>(d, i, S, E);
-        c = is_large(E - S) ? chunk_count(S, E) : 0;
+        c = is_large(E - S) ? chunk_count(S, E, d.cshift) : 0;
     }
     // exclusive scan over the workgroup: in-wave inclusive scan, then waves
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1056,6 +1098,7 @@ __global__ __launch_bounds__(kThreads) void k_plan_scan(Plan pl)
     if (threadIdx.x == 0) {
         carry_s = 0;
         *pl.status = 0;   // stream-ordered before this launch's k_chunks
+        *pl.ticket = 0;
     }
     __syncthreads();
     for (uint64_t base = 0; base < pl.ngroups; base += kThreads) {
@@ -1205,6 +1248,7 @@ Plan make_plan(ramcrc_ctx* c, uint64_t n)
     pl.partials = c->partials;
     pl.partials_cap = c->partials_cap;
     pl.status = c->status;
+    pl.ticket = reinterpret_cast<unsigned long long*>(c->status + 2);   // 8-byte aligned
     return pl;
 }
 
@@ -1466,6 +1510,7 @@ int ramcrc_segments_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_bytes
     DeviceGuard g(c->device);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     BatchDesc d{};
+    d.cshift = kChunkShift;
     d.base = static_cast<const uint8_t*>(d_base);
     d.seg_bytes = seg_bytes;
     d.n = nseg;
@@ -1478,7 +1523,15 @@ int ramcrc_segments_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_bytes
     const uint64_t B = reinterpret_cast<uint64_t>(d_base);
     if ((B % kChunk) == 0 && (seg_bytes % kChunk) == 0) {
         // The recovery-scan fast path: no plan, chunk g -> (g / per, g % per).
-        const uint64_t per = seg_bytes / kChunk;
+        // Largest chunk (256 KiB .. 1 MiB) that still gives every wave two
+        // chunks: fewer per-chunk pipeline drains and folds.
+        const uint64_t waves = uint64_t(c->ncu) * kWavesPerGroup;
+        uint32_t shift = kChunkShift;
+        while (shift < 20 && (B % (2ull << shift)) == 0 && (seg_bytes % (2ull << shift)) == 0 &&
+               (seg_bytes >> (shift + 1)) * nseg >= 2 * waves)
+            shift++;
+        d.cshift = shift;
+        const uint64_t per = seg_bytes >> shift;
         int rc = reserve_locked(c, per * nseg, 1);
         if (rc)
             return rc;
@@ -1514,6 +1567,7 @@ int ramcrc_batch_device(ramcrc_ctx* c, const void* d_base, const uint64_t* d_off
     if (rc)
         return rc;
     BatchDesc d{};
+    d.cshift = kChunkShift;
     d.base = static_cast<const uint8_t*>(d_base);
     d.off = d_off;
     d.len = d_len;
@@ -1536,6 +1590,7 @@ int ramcrc_entries_device(ramcrc_ctx* c, const void* d_base, const uint64_t* d_o
     DeviceGuard g(c->device);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     BatchDesc d{};
+    d.cshift = kChunkShift;
     d.base = static_cast<const uint8_t*>(d_base);
     d.off = d_off;
     d.len = d_len;

@@ -28,7 +28,8 @@ class RamcrcError(RuntimeError):
 
 
 def lib_path():
-    return _build.LIB
+    # RAMCRC_LIB selects a tuning variant built by `python -m ramcloud_amd.build --variants`
+    return os.environ.get("RAMCRC_LIB") or _build.LIB
 
 
 def lib():
@@ -36,7 +37,7 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
-    path = _build.LIB
+    path = lib_path()
     if not os.path.exists(path):
         raise RamcrcError(f"libramcrc.so not built ({path}); run python -m ramcloud_amd.build")
     L = _c.CDLL(path)
