@@ -77,14 +77,13 @@ constexpr int kUnroll = RAMCRC_UNROLL;             // blocks per register group 
 constexpr bool kDynamic = RAMCRC_DYNAMIC;          // waves dequeue chunks from a counter
 
 // ------------------------------------------------------------------ tables
-struct DeviceTables {
+struct alignas(16) DeviceTables {
     OpTable stride_large;   // X^1024: Horner step of k_chunks
     OpTable stride_small;   // X^128:  Horner step of k_entries (8 lanes x 16 B)
     OpTable comb[7];        // X^4, X^16, X^32, X^64, X^128, X^256, X^512
     ramcrc::ByteTable t0;   // X^1 byte step
     uint32_t xblk[4][256];  // x^(8 * 1024 * b * 256^j)
     uint32_t xinv[1024];    // x^(-8 p)
-    uint32_t ecst[8][128];  // k_entries: x^(8 (16 (7 - l) - pad)), lane l of a group
     uint32_t pos[129][256]; // k_entries_tiny: X^m(byte) for m = 0..128
 };
 
@@ -116,11 +115,6 @@ constexpr DeviceTables make_device_tables()
         for (uint32_t b = 0; b < 256; b++)
             t.pos[m][b] = ramcrc::mulmod(b, c);
     }
-    for (int l = 0; l < 8; l++)
-        for (int pad = 0; pad < 128; pad++) {
-            const int d = 16 * (7 - l) - pad;
-            t.ecst[l][pad] = ramcrc::mulmod(t.xinv[d < 0 ? -d : 0], ramcrc::xpow8(d > 0 ? d : 0));
-        }
     return t;
 }
 
@@ -139,33 +133,64 @@ static_assert(ramcrc::mulmod(ramcrc::xpow8(3), ramcrc::xinv8pow(3)) == ramcrc::k
 constexpr uint32_t kRepBytes = 131072;
 constexpr uint32_t kCombOff = kRepBytes;                  // k_chunks: 7 x 4 KiB
 constexpr uint32_t kLdsChunks = kCombOff + 7 * 4096;      // 159744 B
-constexpr uint32_t kX4Off = kRepBytes;                    // k_entries: X^4 (4 KiB)
-constexpr uint32_t kCstOff = kX4Off + 4096;               // k_entries: ecst (4 KiB)
-constexpr uint32_t kT0Off = kCstOff + 4096;               // k_entries: X^1 (1 KiB)
-constexpr uint32_t kBinOff = kT0Off + 1024;               // k_entries: bin table (4 KiB)
-constexpr uint32_t kLdsEntries = kBinOff + 4096;          // 143360 B
+constexpr uint32_t kX4Off = kRepBytes;                    // k_entries: X^4,16,32,64 (16 KiB)
+constexpr uint32_t kXinvOff = kX4Off + 4 * 4096;          // k_entries: x^(-8 pad) (512 B)
+constexpr uint32_t kBinOff = kXinvOff + 512;              // k_entries: bin table (4 KiB)
+constexpr uint32_t kLdsEntries = kBinOff + 4096;          // 152064 B
+static_assert(kLdsEntries <= 160 * 1024, "LDS budget");
 static_assert(kLdsChunks <= 160 * 1024, "LDS budget");
 
+// LDS table fills.  Every thread issues all of its global loads before its
+// first LDS store, so a fill costs about one L2 round trip instead of one per
+// loop iteration (a 129 KiB fill would otherwise serialise ~33 round trips).
 __device__ __forceinline__ void fill_replicated(uint8_t* lds, const OpTable& op)
 {
-    // 4 tables x 256 entries x 32 replicas; each thread writes 4 replicas
-    // (16 contiguous bytes) per iteration.
-    for (uint32_t idx = threadIdx.x; idx < 4 * 256 * 8; idx += blockDim.x) {
-        const uint32_t k = idx >> 11;
-        const uint32_t b = (idx >> 3) & 255;
-        const uint32_t q = idx & 7;
-        const uint32_t v = op.t[k][b];
-        const uint32_t off = (k >> 1) * 65536 + b * 256 + (k & 1) * 128 + q * 16;
-        *reinterpret_cast<uint4*>(lds + off) = make_uint4(v, v, v, v);
+    // 4 tables x 256 entries x 32 replicas; each item writes 4 replicas (16
+    // contiguous bytes): 8192 items.
+    constexpr uint32_t kItems = 4 * 256 * 8;
+    constexpr int kU = 8;
+    for (uint32_t base = threadIdx.x; base < kItems; base += kU * blockDim.x) {
+        uint32_t v[kU];
+#pragma unroll
+        for (int j = 0; j < kU; j++) {
+            const uint32_t idx = base + j * blockDim.x;
+            const uint32_t ci = idx < kItems ? idx : 0;
+            v[j] = op.t[ci >> 11][(ci >> 3) & 255];
+        }
+#pragma unroll
+        for (int j = 0; j < kU; j++) {
+            const uint32_t idx = base + j * blockDim.x;
+            if (idx < kItems) {
+                const uint32_t k = idx >> 11, bv = (idx >> 3) & 255, q = idx & 7;
+                const uint32_t off = (k >> 1) * 65536 + bv * 256 + (k & 1) * 128 + q * 16;
+                *reinterpret_cast<uint4*>(lds + off) = make_uint4(v[j], v[j], v[j], v[j]);
+            }
+        }
     }
 }
 
+// words % 4 == 0; src and lds + off 16-byte aligned.
 __device__ __forceinline__ void fill_plain(uint8_t* lds, uint32_t off, const uint32_t* src,
                                            uint32_t words)
 {
-    uint32_t* dst = reinterpret_cast<uint32_t*>(lds + off);
-    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x)
-        dst[i] = src[i];
+    const uint4* s = reinterpret_cast<const uint4*>(src);
+    uint4* dst = reinterpret_cast<uint4*>(lds + off);
+    const uint32_t n = words / 4;
+    constexpr int kU = 9;
+    for (uint32_t base = threadIdx.x; base < n; base += kU * blockDim.x) {
+        uint4 v[kU];
+#pragma unroll
+        for (int j = 0; j < kU; j++) {
+            const uint32_t i = base + j * blockDim.x;
+            v[j] = s[i < n ? i : 0];
+        }
+#pragma unroll
+        for (int j = 0; j < kU; j++) {
+            const uint32_t i = base + j * blockDim.x;
+            if (i < n)
+                dst[i] = v[j];
+        }
+    }
 }
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
@@ -230,6 +255,20 @@ __device__ __forceinline__ uint32_t mulmod_dev(uint32_t a, uint32_t b)
     for (int i = 0; i < 32; i++) {
         p ^= (a & (0x80000000u >> i)) ? b : 0u;
         b = (b >> 1) ^ ((b & 1u) ? ramcrc::kPoly : 0u);
+    }
+    return p;
+}
+
+// Same product, Horner over the bits of a (highest power first): one running
+// register, for call sites where register pressure matters more than latency.
+__device__ __forceinline__ uint32_t mulmod_horner(uint32_t a, uint32_t b)
+{
+    uint32_t p = 0;
+#pragma unroll
+    for (int j = 0; j < 32; j++) {
+        const uint32_t ma = uint32_t(int32_t(a << (31 - j)) >> 31);   // coefficient of x^(31-j)
+        const uint32_t mp = 0u - (p & 1u);
+        p = (p >> 1) ^ (mp & ramcrc::kPoly) ^ (ma & b);
     }
     return p;
 }
@@ -575,9 +614,11 @@ __global__ __launch_bounds__(256) void k_combine(BatchDesc d, Plan pl, uint64_t 
 constexpr int kG = 8;                      // lanes per entry group
 constexpr uint64_t kStep = kG * 16;        // bytes per group step
 constexpr int kNB = 161;                   // step-count bins
+constexpr int kSmallK = 4;                 // bins 2..kSmallK: octets loaded one ahead
 constexpr int kPU = 4;                     // ping-pong depth (pipelined bins)
 constexpr uint32_t kNoIdx = 0xFFFFFFFFu;   // empty slot
-constexpr uint64_t kOctetCost = 3;         // per-octet overhead in step units (work split)
+constexpr uint64_t kOctetCost = 4;         // per-octet overhead in step units (work split)
+constexpr int kBinPer = 4;                 // entries per thread per tile (count/scatter)
 constexpr uint32_t kLdsTiny = 129 * 1024;  // k_entries_tiny: X^m(byte), m = 0..128
 
 struct BinTable {
@@ -585,7 +626,9 @@ struct BinTable {
     uint64_t count[kNB];      // entries in the bin
     uint64_t items[kNB + 1];  // exclusive prefix of octets * kmax: work units
     uint64_t cursor[kNB];     // scatter cursors
+    uint64_t kcost[kNB];      // steps charged per octet of the bin (observed max)
     uint32_t hist[kNB];       // entry counts; zero between launches
+    uint32_t kobs[kNB];       // observed max steps (log-scale bins); zero between launches
 };
 
 struct Sorted {
@@ -621,58 +664,130 @@ __device__ __forceinline__ uint64_t bin_kmax(int b)
     return (uint64_t(5 + f) << (m - 2)) - 1;
 }
 
+// One LDS atomic per distinct bin of a wave instead of one per lane (log
+// entries fall into a handful of bins, so per-lane atomics serialise).
+// Returns this lane's rank among the wave's lanes of the same bin; *base_lane
+// receives the previous counter value for the lane's bin.
+__device__ __forceinline__ uint32_t wave_bin_add(uint32_t* h, int b, bool active, uint32_t& base)
+{
+    uint64_t todo = __ballot(active);
+    const int lane = threadIdx.x & (kWaveSize - 1);
+    uint32_t rank = 0;
+    base = 0;
+    while (todo) {
+        const int leader = int(__builtin_ctzll(todo));
+        const int lb = __shfl(b, leader, kWaveSize);
+        const uint64_t same = __ballot(active && b == lb);
+        uint32_t old = 0;
+        if (lane == leader)
+            old = atomicAdd(&h[lb], uint32_t(__popcll(same)));
+        old = __shfl(old, leader, kWaveSize);
+        if (active && b == lb) {
+            base = old;
+            rank = uint32_t(__popcll(same & ((1ull << lane) - 1)));
+        }
+        todo &= ~same;
+    }
+    return rank;
+}
+
 template <int kMode>
 __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, int skip_large)
 {
-    __shared__ uint32_t h[kNB];
+    __shared__ uint32_t h[kNB], kmx[kNB];
     for (int t = threadIdx.x; t < kNB; t += blockDim.x)
-        h[t] = 0;
+        h[t] = kmx[t] = 0;
     __syncthreads();
-    const uint64_t nthreads = uint64_t(gridDim.x) * blockDim.x;
-    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < d.n; i += nthreads) {
-        uint64_t S, E;
-        buffer_range<kMode>(d, i, S, E);
-        if (skip_large && is_large(E - S))
-            continue;
-        atomicAdd(&h[bin_of(S, E)], 1u);
+    const uint64_t tile = uint64_t(blockDim.x) * kBinPer;
+    for (uint64_t base = uint64_t(blockIdx.x) * tile; base < d.n; base += uint64_t(gridDim.x) * tile) {
+        uint64_t S[kBinPer], E[kBinPer];
+#pragma unroll
+        for (int q = 0; q < kBinPer; q++) {   // all loads first
+            const uint64_t i = base + uint64_t(q) * blockDim.x + threadIdx.x;
+            S[q] = E[q] = 0;
+            if (i < d.n)
+                buffer_range<kMode>(d, i, S[q], E[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < kBinPer; q++) {
+            const uint64_t i = base + uint64_t(q) * blockDim.x + threadIdx.x;
+            const bool active = i < d.n && !(skip_large && is_large(E[q] - S[q]));
+            const int b = active ? bin_of(S[q], E[q]) : 0;
+            if (active && b > 32)
+                atomicMax(&kmx[b], uint32_t(entry_steps(S[q], E[q])));
+            uint32_t unused;
+            wave_bin_add(h, b, active, unused);
+        }
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < kNB; t += blockDim.x)
+    for (int t = threadIdx.x; t < kNB; t += blockDim.x) {
         if (h[t])
             atomicAdd(&so.bt->hist[t], h[t]);
+        if (kmx[t])
+            atomicMax(&so.bt->kobs[t], kmx[t]);
+    }
 }
 
 __global__ __launch_bounds__(256) void k_bin_scan(Sorted so)
 {
+    // 256 threads, one bin each: parallel exclusive scans of the slot counts
+    // and of the work units (no serial loop, no dependent global round trips).
+    __shared__ uint64_t wpos[4], witem[4];
     __shared__ uint64_t s_start[kNB], s_count[kNB];
     BinTable* bt = so.bt;
-    if (threadIdx.x == 0) {
-        uint64_t pos = 0, items = 0;
-        for (int b = 0; b < kNB; b++) {
-            const uint64_t c = bt->hist[b];
-            const uint64_t oct = (c + kG - 1) / kG;
-            bt->start[b] = pos;
-            bt->count[b] = c;
-            bt->cursor[b] = pos;
-            bt->items[b] = items;
-            bt->hist[b] = 0;
-            s_start[b] = pos;
-            s_count[b] = c;
-            pos += oct * kG;
-            if (b >= 2)   // bins 0-1 belong to k_entries_tiny
-                items += oct * (bin_kmax(b) + kOctetCost);
-        }
-        bt->items[kNB] = items;
+    const int b = threadIdx.x, lane = b & 63, w = b >> 6;
+    uint64_t cnt = 0, kc = 0;
+    if (b < kNB) {
+        cnt = bt->hist[b];
+        const uint32_t ko = bt->kobs[b];
+        kc = b <= 32 ? uint64_t(b == 0 ? 1 : b) : (ko ? ko : bin_kmax(b));
+        bt->hist[b] = 0;   // ready for the next launch (stream-ordered)
+        bt->kobs[b] = 0;
     }
+    const uint64_t oct = (cnt + kG - 1) / kG;
+    const uint64_t pos_c = oct * kG;
+    const uint64_t item_c = b >= 2 ? oct * (kc + kOctetCost) : 0;   // bins 0-1: tiny kernel
+    uint64_t ps = pos_c, is = item_c;
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+        const uint64_t a1 = __shfl_up(ps, s, kWaveSize);
+        const uint64_t a2 = __shfl_up(is, s, kWaveSize);
+        if (lane >= s) {
+            ps += a1;
+            is += a2;
+        }
+    }
+    if (lane == 63) {
+        wpos[w] = ps;
+        witem[w] = is;
+    }
+    __syncthreads();
+    uint64_t pb = 0, ib = 0;
+    for (int j = 0; j < w; j++) {
+        pb += wpos[j];
+        ib += witem[j];
+    }
+    const uint64_t start = pb + ps - pos_c, items = ib + is - item_c;
+    if (b < kNB) {
+        bt->start[b] = start;
+        bt->count[b] = cnt;
+        bt->cursor[b] = start;
+        bt->items[b] = items;
+        bt->kcost[b] = kc + kOctetCost;
+        s_start[b] = start;
+        s_count[b] = cnt;
+    }
+    if (b == kNB - 1)
+        bt->items[kNB] = items + item_c;
     __syncthreads();
     // padding slots of each bin's last octet: empty
     for (int t = threadIdx.x; t < kNB * kG; t += blockDim.x) {
-        const int b = t / kG, j = t % kG;
-        const uint64_t c = s_count[b];
+        const int bb = t / kG, j = t % kG;
+        const uint64_t c = s_count[bb];
         const uint64_t slot = c + uint64_t(j);
         if ((c % kG) && slot < (c + kG - 1) / kG * kG) {
-            so.desc[s_start[b] + slot] = u32x4{0u, 0u, 0u, 0u};
-            so.idx[s_start[b] + slot] = kNoIdx;
+            so.desc[s_start[bb] + slot] = u32x4{0u, 0u, 0u, 0u};
+            so.idx[s_start[bb] + slot] = kNoIdx;
         }
     }
 }
@@ -685,18 +800,28 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter(BatchDesc d, Sorted so
     for (int t = threadIdx.x; t < kNB; t += blockDim.x)
         cnt[t] = 0;
     __syncthreads();
-    for (uint64_t tile = uint64_t(blockIdx.x) * blockDim.x; tile < d.n;
-         tile += uint64_t(gridDim.x) * blockDim.x) {
-        const uint64_t i = tile + threadIdx.x;
-        int b = -1;
-        uint32_t lp = 0;
-        uint64_t S = 0, E = 0;
-        if (i < d.n) {
-            buffer_range<kMode>(d, i, S, E);
-            if (!(skip_large && is_large(E - S))) {
-                b = bin_of(S, E);
-                lp = atomicAdd(&cnt[b], 1u);
-            }
+    const uint64_t tile = uint64_t(blockDim.x) * kBinPer;
+    for (uint64_t t0 = uint64_t(blockIdx.x) * tile; t0 < d.n; t0 += uint64_t(gridDim.x) * tile) {
+        uint64_t S[kBinPer], E[kBinPer];
+        int b[kBinPer];
+        uint32_t lp[kBinPer];
+#pragma unroll
+        for (int q = 0; q < kBinPer; q++) {
+            const uint64_t i = t0 + uint64_t(q) * blockDim.x + threadIdx.x;
+            S[q] = E[q] = 0;
+            if (i < d.n)
+                buffer_range<kMode>(d, i, S[q], E[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < kBinPer; q++) {
+            const uint64_t i = t0 + uint64_t(q) * blockDim.x + threadIdx.x;
+            const bool active = i < d.n && !(skip_large && is_large(E[q] - S[q]));
+            b[q] = active ? bin_of(S[q], E[q]) : 0;
+            uint32_t wbase;
+            const uint32_t rank = wave_bin_add(cnt, b[q], active, wbase);
+            lp[q] = wbase + rank;
+            if (!active)
+                b[q] = -1;
         }
         __syncthreads();
         for (int t = threadIdx.x; t < kNB; t += blockDim.x)
@@ -706,12 +831,17 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter(BatchDesc d, Sorted so
                 cnt[t] = 0;
             }
         __syncthreads();
-        if (b >= 0) {
-            const uint64_t pos = base[b] + lp;
-            so.desc[pos] = u32x4{uint32_t(S), uint32_t(S >> 32), uint32_t(E), uint32_t(E >> 32)};
-            so.idx[pos] = uint32_t(i);
-            if (d.init)
-                so.init[pos] = d.init[i];
+#pragma unroll
+        for (int q = 0; q < kBinPer; q++) {
+            if (b[q] >= 0) {
+                const uint64_t i = t0 + uint64_t(q) * blockDim.x + threadIdx.x;
+                const uint64_t pos = base[b[q]] + lp[q];
+                so.desc[pos] = u32x4{uint32_t(S[q]), uint32_t(S[q] >> 32), uint32_t(E[q]),
+                                     uint32_t(E[q] >> 32)};
+                so.idx[pos] = uint32_t(i);
+                if (d.init)
+                    so.init[pos] = d.init[i];
+            }
         }
         __syncthreads();
     }
@@ -754,37 +884,42 @@ __device__ __forceinline__ u32x4 fix_piece(u32x4 w, uint64_t a, uint64_t S, uint
     return w;
 }
 
-// End of an entry: fold the slots, move to the entry end, XOR the group.
-// Every lane of the group returns the entry's raw state.
-__device__ __forceinline__ uint32_t entry_finish(const uint8_t* lds, int gl, uint32_t u0,
-                                                 uint32_t u1, uint32_t u2, uint32_t u3,
-                                                 uint64_t S, uint64_t E, uint64_t steps,
-                                                 uint32_t init)
+// Lane piece -> window end: fold the four word slots with X^4, then the
+// group's eight lanes with X^16, X^32, X^64 (a shuffle butterfly).  Every lane
+// of the group returns the entry's raw state relative to the end of its last
+// 128-byte window; the caller removes the zero padding with x^(-8 pad).
+__device__ __forceinline__ uint32_t group_fold(const uint8_t* lds, int gl, uint32_t u0,
+                                               uint32_t u1, uint32_t u2, uint32_t u3)
 {
-    uint32_t R;
-    if (E - S >= 4) {
-        uint32_t y = plain_apply(lds, kX4Off, u0) ^ u1;
-        y = plain_apply(lds, kX4Off, y) ^ u2;
-        y = plain_apply(lds, kX4Off, y) ^ u3;
-        y = plain_apply(lds, kX4Off, y);
-        const uint64_t B = (S & ~uint64_t(15)) + steps * kStep;
-        const uint32_t pad = uint32_t(B - E);   // < 128
-        const uint32_t* cst = reinterpret_cast<const uint32_t*>(lds + kCstOff);
-        R = mulmod_dev(y, cst[gl * 128 + pad]);
-    } else {
-        // 0-3 bytes: byte steps from the initial state (lane 0 of the group)
-        R = 0;
-        if (gl == 0) {
-            R = init;
-            const uint32_t* t0 = reinterpret_cast<const uint32_t*>(lds + kT0Off);
-            for (uint64_t a = S; a < E; a++)
-                R = t0[(R ^ *(const gu8*)a) & 0xFF] ^ (R >> 8);
-        }
+    uint32_t z = plain_apply(lds, kX4Off, u0) ^ u1;
+    z = plain_apply(lds, kX4Off, z) ^ u2;
+    z = plain_apply(lds, kX4Off, z) ^ u3;
+    z = plain_apply(lds, kX4Off, z);
+#pragma unroll
+    for (int lvl = 0; lvl < 3; lvl++) {
+        const uint32_t other = __shfl_xor(z, 1 << lvl, kWaveSize);
+        const bool upper = (gl >> lvl) & 1;
+        const uint32_t lower_v = upper ? other : z;
+        const uint32_t upper_v = upper ? z : other;
+        z = plain_apply(lds, kX4Off + (1 + lvl) * 4096, lower_v) ^ upper_v;
     }
-    R ^= __shfl_xor(R, 1, kWaveSize);
-    R ^= __shfl_xor(R, 2, kWaveSize);
-    R ^= __shfl_xor(R, 4, kWaveSize);
-    return R;
+    return z;
+}
+
+// Head word at distance ds = S - (word address): drop the bytes before S and
+// inject the initial state into the four bytes at S.
+__device__ __forceinline__ uint32_t keep_lo(int c);
+__device__ __forceinline__ uint32_t head_word(uint32_t w, int ds, uint32_t init)
+{
+    const uint32_t inj = uint32_t((uint64_t(init) << 24) >> (24 - 8 * min(max(ds, -3), 3)));
+    return (w & ~keep_lo(ds)) ^ ((ds > -4 && ds < 4) ? inj : 0u);
+}
+
+// Byte mask of a word whose first c bytes (clamped to 0..4) are kept.
+__device__ __forceinline__ uint32_t keep_lo(int c)
+{
+    c = min(max(c, 0), 4);
+    return c >= 4 ? 0xFFFFFFFFu : (1u << (8 * c)) - 1u;
 }
 
 // Entries of at most one 128-byte window (bins 0-1; 100-byte log entries are
@@ -795,6 +930,8 @@ __device__ __forceinline__ uint32_t entry_finish(const uint8_t* lds, int gl, uin
 __global__ __launch_bounds__(kThreads, 1) void k_entries_tiny(BatchDesc d, Sorted so)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsTiny];
+    if (so.bt->start[2] == so.bt->start[0])
+        return;   // no entry of at most one window (uniform: every wave exits)
     fill_plain(lds, 0, &g_tab.pos[0][0], 129 * 256);
     __syncthreads();
     const uint32_t* tab = reinterpret_cast<const uint32_t*>(lds);
@@ -870,24 +1007,43 @@ __global__ __launch_bounds__(kThreads, 1) void k_entries_tiny(BatchDesc d, Sorte
 }
 
 // Entries of two or more 128-byte steps (bins >= 2).  One octet (8 entries,
-// one per lane group) at a time, kPU-deep ping-pong prefetch of the steps, the
-// next octet's descriptor prefetched during the current one.  Waves split the
-// bins by estimated work (steps + kOctetCost per octet).
+// one per lane group) at a time:
+//   step 0 (head)          start mask and init injection, precomputed per octet;
+//   steps 1 .. Kmin-2      interior for every entry of the octet: no masks,
+//                          unconditional loads, kPU-deep ping-pong prefetch;
+//   steps Kmin-1 .. Koct-1 tail: end mask, lanes past their entry frozen.
+// The head and the first two tail loads are issued with the interior ones, the
+// next octet's descriptor is prefetched, and the previous octet's fold runs
+// after this octet's loads are in flight.  The unpad multiply x^(-8 pad) is
+// batched: lane gl of a group keeps the fold of octet gl of the current eight,
+// and one wave-wide multiply finishes 64 entries.  Waves split the bins by
+// estimated work (steps + kOctetCost per octet).
+//
+// kSmall: bins 2 .. kSmallK (whole octets loaded one ahead); otherwise bins
+// kSmallK+1 and up.  Two instantiations keep the register allocation of the
+// long-entry loop free of the short-entry loop's state.
+template <bool kSmall>
 __global__ __launch_bounds__(kThreads, 1) void k_entries(BatchDesc d, Sorted so)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsEntries];
+    constexpr int b0 = kSmall ? 2 : kSmallK + 1, b1 = kSmall ? kSmallK + 1 : kNB;
+    if (so.bt->items[b0] == so.bt->items[b1])
+        return;   // no entry in this kernel's bins
     fill_replicated(lds, g_tab.stride_small);
-    fill_plain(lds, kX4Off, &g_tab.comb[0].t[0][0], 1024);
-    fill_plain(lds, kCstOff, &g_tab.ecst[0][0], 1024);
-    fill_plain(lds, kT0Off, g_tab.t0.t, 256);
+    fill_plain(lds, kX4Off, &g_tab.comb[0].t[0][0], 4 * 1024);
+    fill_plain(lds, kXinvOff, g_tab.xinv, 128);
     uint64_t* s_items = reinterpret_cast<uint64_t*>(lds + kBinOff);   // kNB + 1
     uint64_t* s_start = s_items + (kNB + 1);                          // kNB
+    uint32_t* s_cost = reinterpret_cast<uint32_t*>(s_start + kNB);    // kNB
     for (int t = threadIdx.x; t <= kNB; t += blockDim.x) {
         s_items[t] = so.bt->items[t];
-        if (t < kNB)
+        if (t < kNB) {
             s_start[t] = so.bt->start[t];
+            s_cost[t] = uint32_t(so.bt->kcost[t]);
+        }
     }
     __syncthreads();
+    const uint32_t* xinv = reinterpret_cast<const uint32_t*>(lds + kXinvOff);
 
     const int lane = threadIdx.x & (kWaveSize - 1);
     const int g = lane >> 3, gl = lane & 7;
@@ -895,23 +1051,126 @@ __global__ __launch_bounds__(kThreads, 1) void k_entries(BatchDesc d, Sorted so)
     const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerGroup +
                           __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
     const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerGroup;
-    const uint64_t T = s_items[kNB];
-    const uint64_t lo = T * wave / nwaves, hi = T * (wave + 1) / nwaves;
+    const uint64_t I0 = s_items[b0], T = s_items[b1] - I0;
+    const uint64_t lo = I0 + T * wave / nwaves, hi = I0 + T * (wave + 1) / nwaves;
     const bool finalize = d.flags & RAMCRC_FINALIZE;
     const uint64_t dummy = reinterpret_cast<uint64_t>(so.bt);   // device memory, 16 B aligned
 
-    for (int b = 2; b < kNB; b++) {
+    // batched unpad: lane gl holds octet gl of the current batch of eight
+    uint32_t bY = 0, bPad = 0, bIx = kNoIdx;
+    int nb = 0;
+    auto flush_batch = [&]() {
+        const uint32_t R = mulmod_horner(bY, xinv[bPad & 127]);
+        if (bIx != kNoIdx)
+            d.out[bIx] = finalize ? ~R : R;
+        bIx = kNoIdx;
+        nb = 0;
+    };
+    // deferred fold of the previous octet
+    bool pend = false;
+    uint32_t pu0 = 0, pu1 = 0, pu2 = 0, pu3 = 0, ppad = 0, pix = kNoIdx;
+    auto flush = [&]() {
+        if (pend) {
+            const uint32_t Y = group_fold(lds, gl, pu0, pu1, pu2, pu3);
+            if (gl == nb) {
+                bY = Y;
+                bPad = ppad;
+                bIx = pix;
+            }
+            pend = false;
+            if (++nb == kG)
+                flush_batch();
+        }
+    };
+
+    for (int b = b0; b < b1; b++) {
         const uint64_t ib = s_items[b], ie = s_items[b + 1];
         if (ie <= lo || ib == ie)
             continue;
         if (ib >= hi)
             break;
-        const uint64_t cost = bin_kmax(b) + kOctetCost;
+        const uint64_t cost = s_cost[b];
         const uint64_t oa = ((lo > ib ? lo : ib) - ib + cost - 1) / cost;
         const uint64_t ob = ((hi < ie ? hi : ie) - ib + cost - 1) / cost;
         const uint64_t sb = s_start[b];
         if (oa >= ob)
             continue;
+        if constexpr (kSmall) {
+            // Exact bins of at most kSmallK steps: the whole octet is loaded
+            // one octet ahead, so the load latency hides behind the previous
+            // octet's steps and fold instead of stalling every octet.
+            const uint32_t K = uint32_t(b);
+            struct Oct {
+                uint64_t S, E;
+                uint32_t init, ix, steps;
+                u32x4 w[kSmallK];
+            };
+            auto load_oct = [&](uint64_t o, Oct& t) {
+                const uint64_t sl = sb + o * kG + g;
+                const u32x4 dd = so.desc[sl];
+                t.ix = so.idx[sl];
+                t.init = d.init ? so.init[sl] : 0xFFFFFFFFu;
+                t.S = (uint64_t(dd.y) << 32) | dd.x;
+                t.E = (uint64_t(dd.w) << 32) | dd.z;
+                t.steps = t.ix != kNoIdx ? K : 0u;
+                const uint64_t A = t.S & ~uint64_t(15);
+                const uint64_t p0 = A + gl * 16;
+                const uint64_t safe = t.steps ? A : dummy;
+#pragma unroll
+                for (int k = 0; k < kSmallK; k++) {
+                    const uint64_t a = p0 + uint64_t(k) * kStep;
+                    if (k < int(K))
+                        t.w[k] = load16(t.steps && a < t.E ? a : safe);
+                }
+            };
+            Oct cur, nxt;
+            load_oct(oa, cur);
+            for (uint64_t o = oa; o < ob; o++) {
+                if (o + 1 < ob)
+                    load_oct(o + 1, nxt);
+                const uint64_t A = cur.S & ~uint64_t(15);
+                const uint64_t p0 = A + gl * 16;
+                uint32_t u0 = 0, u1 = 0, u2 = 0, u3 = 0;
+                {
+                    const int off = int(uint32_t(cur.S - A)) - 16 * gl;
+                    u32x4 w = cur.w[0];
+                    w.x = head_word(w.x, off, cur.init);
+                    w.y = head_word(w.y, off - 4, cur.init);
+                    w.z = head_word(w.z, off - 8, cur.init);
+                    w.w = head_word(w.w, off - 12, cur.init);
+                    u0 = op.apply(lds, u0, w.x);
+                    u1 = op.apply(lds, u1, w.y);
+                    u2 = op.apply(lds, u2, w.z);
+                    u3 = op.apply(lds, u3, w.w);
+                }
+                const int64_t erel = int64_t(cur.E - p0);
+#pragma unroll
+                for (int k = 1; k < kSmallK; k++) {
+                    if (k < int(K)) {
+                        const int64_t de64 = erel - int64_t(k) * int64_t(kStep);
+                        const int de = int(de64 < 0 ? 0 : (de64 > 16 ? 16 : de64));
+                        u32x4 w = cur.w[k];
+                        w.x &= keep_lo(de);
+                        w.y &= keep_lo(de - 4);
+                        w.z &= keep_lo(de - 8);
+                        w.w &= keep_lo(de - 12);
+                        u0 = op.apply(lds, u0, w.x);
+                        u1 = op.apply(lds, u1, w.y);
+                        u2 = op.apply(lds, u2, w.z);
+                        u3 = op.apply(lds, u3, w.w);
+                    }
+                }
+                pend = true;
+                pu0 = u0;
+                pu1 = u1;
+                pu2 = u2;
+                pu3 = u3;
+                ppad = uint32_t((A + uint64_t(K) * kStep) - cur.E);
+                pix = cur.ix;
+                flush();
+                cur = nxt;
+            }
+        } else {
         u32x4 nd = so.desc[sb + oa * kG + g];
         uint32_t nix = so.idx[sb + oa * kG + g];
         uint32_t ninit = d.init ? so.init[sb + oa * kG + g] : 0xFFFFFFFFu;
@@ -927,29 +1186,97 @@ __global__ __launch_bounds__(kThreads, 1) void k_entries(BatchDesc d, Sorted so)
             }
             const uint64_t S = (uint64_t(dd.y) << 32) | dd.x;
             const uint64_t E = (uint64_t(dd.w) << 32) | dd.z;
-            const uint64_t steps = (ix != kNoIdx && E - S >= 4) ? entry_steps(S, E) : 0;
+            const uint32_t steps = ix != kNoIdx ? uint32_t(entry_steps(S, E)) : 0u;
             const uint64_t A = S & ~uint64_t(15);
             const uint64_t p0 = A + gl * 16;
             // longest / shortest entry of the octet (padding slots excluded)
-            uint32_t kmax32 = uint32_t(steps), kmin32 = steps ? uint32_t(steps) : 0xFFFFFFFFu;
+            uint32_t kmax32 = steps, kmin32 = steps ? steps : 0xFFFFFFFFu;
 #pragma unroll
             for (int s = 8; s < 64; s <<= 1) {
                 kmax32 = max(kmax32, uint32_t(__shfl_xor(kmax32, s, kWaveSize)));
                 kmin32 = min(kmin32, uint32_t(__shfl_xor(kmin32, s, kWaveSize)));
             }
-            const uint64_t Koct = __builtin_amdgcn_readfirstlane(kmax32);
-            const uint64_t Kmin = __builtin_amdgcn_readfirstlane(kmin32);
-            const uint64_t safe = steps ? A : dummy;   // steps == 0: padding slot
-            auto ldk = [&](uint64_t k) -> u32x4 {
-                const uint64_t a = p0 + k * kStep;
-                const bool ok = k < steps && a < E && a + 16 > S;
-                const u32x4 v = load16(ok ? a : safe);
-                return ok ? v : u32x4{0u, 0u, 0u, 0u};
+            const uint32_t Koct = __builtin_amdgcn_readfirstlane(kmax32);
+            const uint32_t Kmin = __builtin_amdgcn_readfirstlane(kmin32);   // >= 2
+            const uint32_t kt0 = Kmin - 1;   // first tail step (>= 1)
+            const uint64_t safe = steps ? A : dummy;
+
+            // loads: head, first two tail steps, first kPU interior steps
+            const gu32x4* pb = gptr16(steps ? p0 : dummy);
+            const uint64_t bstride = steps ? kStep / 16 : 0;
+            auto ldf = [&](uint64_t k) -> u32x4 { return __builtin_nontemporal_load(pb + k * bstride); };
+            auto ldt = [&](uint32_t k) -> u32x4 {   // tail step: lanes past E read a safe word
+                const uint64_t a = p0 + uint64_t(k) * kStep;
+                return load16(k < steps && a < E ? a : safe);
             };
+            const u32x4 wh = ldf(0);
+            const u32x4 wt0 = ldt(kt0);
+            const u32x4 wt1 = ldt(kt0 + 1 < Koct ? kt0 + 1 : kt0);
+            u32x4 Abuf[kPU], Bbuf[kPU];
+#pragma unroll
+            for (int j = 0; j < kPU; j++)
+                Abuf[j] = ldf(1 + j < kt0 ? 1 + j : 0);
+            __builtin_amdgcn_sched_barrier(0);
+            flush();
+
             uint32_t u0 = 0, u1 = 0, u2 = 0, u3 = 0;
-            auto stepk = [&](u32x4 w, uint64_t k) {
-                w = fix_piece(w, p0 + k * kStep, S, E, init);
-                const bool live = k < steps;
+            auto stepf = [&](const u32x4& w) {
+                u0 = op.apply(lds, u0, w.x);
+                u1 = op.apply(lds, u1, w.y);
+                u2 = op.apply(lds, u2, w.z);
+                u3 = op.apply(lds, u3, w.w);
+            };
+            // head: keep bytes >= S, inject init at S .. S+3
+            {
+                const int off = int(uint32_t(S - A)) - 16 * gl;   // S - p0
+                u32x4 w = wh;
+                w.x = head_word(w.x, off, init);
+                w.y = head_word(w.y, off - 4, init);
+                w.z = head_word(w.z, off - 8, init);
+                w.w = head_word(w.w, off - 12, init);
+                stepf(w);
+            }
+            // interior
+            uint32_t k = 1;
+            for (; k + 2 * kPU <= kt0; k += 2 * kPU) {
+#pragma unroll
+                for (int j = 0; j < kPU; j++)
+                    Bbuf[j] = ldf(k + kPU + j);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int j = 0; j < kPU; j++)
+                    stepf(Abuf[j]);
+#pragma unroll
+                for (int j = 0; j < kPU; j++)
+                    Abuf[j] = ldf(k + 2 * kPU + j < kt0 ? k + 2 * kPU + j : 0);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int j = 0; j < kPU; j++)
+                    stepf(Bbuf[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < kPU; j++)
+                if (k + j < kt0)
+                    stepf(Abuf[j]);
+            if (k + kPU < kt0) {
+#pragma unroll
+                for (int j = 0; j < kPU; j++)
+                    Bbuf[j] = ldf(k + kPU + j < kt0 ? k + kPU + j : 0);
+#pragma unroll
+                for (int j = 0; j < kPU; j++)
+                    if (k + kPU + j < kt0)
+                        stepf(Bbuf[j]);
+            }
+            // tail: keep bytes < E; lanes whose entry has ended stay frozen
+            const int64_t erel = int64_t(E - p0);
+            auto stept = [&](u32x4 w, uint32_t kk) {
+                const int64_t de64 = erel - int64_t(kk) * int64_t(kStep);
+                const int de = int(de64 < 0 ? 0 : (de64 > 16 ? 16 : de64));
+                w.x &= keep_lo(de);
+                w.y &= keep_lo(de - 4);
+                w.z &= keep_lo(de - 8);
+                w.w &= keep_lo(de - 12);
+                const bool live = kk < steps;
                 const uint32_t v0 = op.apply(lds, u0, w.x), v1 = op.apply(lds, u1, w.y);
                 const uint32_t v2 = op.apply(lds, u2, w.z), v3 = op.apply(lds, u3, w.w);
                 u0 = live ? v0 : u0;
@@ -957,103 +1284,25 @@ __global__ __launch_bounds__(kThreads, 1) void k_entries(BatchDesc d, Sorted so)
                 u2 = live ? v2 : u2;
                 u3 = live ? v3 : u3;
             };
-            // Steps 1 .. Kmin-2 are interior for every live group: no masks,
-            // no init, unconditional loads (padding groups read their safe word
-            // and their accumulators are never stored).
-            const gu32x4* pb = gptr16(steps ? p0 : dummy);
-            const uint64_t bstride = steps ? kStep / 16 : 0;
-            auto ldf = [&](uint64_t k) -> u32x4 { return __builtin_nontemporal_load(pb + k * bstride); };
-            auto stepf = [&](const u32x4& w) {
-                u0 = op.apply(lds, u0, w.x);
-                u1 = op.apply(lds, u1, w.y);
-                u2 = op.apply(lds, u2, w.z);
-                u3 = op.apply(lds, u3, w.w);
-            };
-            if (Kmin != 0xFFFFFFFFull && Kmin >= 3 && Koct - Kmin <= 1) {
-                const uint64_t kb = Kmin - 1;          // body = [1, kb)
-                const u32x4 wh = ldk(0);
-                const u32x4 wt0 = ldk(kb);
-                const u32x4 wt1 = ldk(kb + 1 < Koct ? kb + 1 : kb);
-                u32x4 Abuf[kPU], Bbuf[kPU];
-#pragma unroll
-                for (int j = 0; j < kPU; j++)
-                    Abuf[j] = ldf(1 + j < kb ? 1 + j : kb - 1);
-                stepk(wh, 0);
-                uint64_t k = 1;
-                for (; k + 2 * kPU <= kb; k += 2 * kPU) {
-#pragma unroll
-                    for (int j = 0; j < kPU; j++)
-                        Bbuf[j] = ldf(k + kPU + j);
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int j = 0; j < kPU; j++)
-                        stepf(Abuf[j]);
-#pragma unroll
-                    for (int j = 0; j < kPU; j++)
-                        Abuf[j] = ldf(k + 2 * kPU + j < kb ? k + 2 * kPU + j : kb - 1);
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int j = 0; j < kPU; j++)
-                        stepf(Bbuf[j]);
-                }
-#pragma unroll
-                for (int j = 0; j < kPU; j++)
-                    if (k + j < kb)
-                        stepf(Abuf[j]);
-                if (k + kPU < kb) {
-#pragma unroll
-                    for (int j = 0; j < kPU; j++)
-                        Bbuf[j] = ldf(k + kPU + j < kb ? k + kPU + j : kb - 1);
-#pragma unroll
-                    for (int j = 0; j < kPU; j++)
-                        if (k + kPU + j < kb)
-                            stepf(Bbuf[j]);
-                }
-                stepk(wt0, kb);
-                if (kb + 1 < Koct)
-                    stepk(wt1, kb + 1);
-            } else {
-                // ragged octet (log-scale bins): every step checked
-                u32x4 Abuf[kPU], Bbuf[kPU];
-#pragma unroll
-                for (int j = 0; j < kPU; j++)
-                    Abuf[j] = ldk(j);
-                uint64_t k = 0;
-                for (; k + 2 * kPU <= Koct; k += 2 * kPU) {
-#pragma unroll
-                    for (int j = 0; j < kPU; j++)
-                        Bbuf[j] = ldk(k + kPU + j);
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int j = 0; j < kPU; j++)
-                        stepk(Abuf[j], k + j);
-#pragma unroll
-                    for (int j = 0; j < kPU; j++)
-                        Abuf[j] = ldk(k + 2 * kPU + j);
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int j = 0; j < kPU; j++)
-                        stepk(Bbuf[j], k + kPU + j);
-                }
-#pragma unroll
-                for (int j = 0; j < kPU; j++)
-                    if (k + j < Koct)
-                        stepk(Abuf[j], k + j);
-                if (k + kPU < Koct) {
-#pragma unroll
-                    for (int j = 0; j < kPU; j++)
-                        Bbuf[j] = ldk(k + kPU + j);
-#pragma unroll
-                    for (int j = 0; j < kPU; j++)
-                        if (k + kPU + j < Koct)
-                            stepk(Bbuf[j], k + kPU + j);
-                }
-            }
-            const uint32_t R = entry_finish(lds, gl, u0, u1, u2, u3, S, E, steps, init);
-            if (gl == 0 && ix != kNoIdx)
-                d.out[ix] = finalize ? ~R : R;
+            stept(wt0, kt0);
+            if (kt0 + 1 < Koct)
+                stept(wt1, kt0 + 1);
+            for (uint32_t kk = kt0 + 2; kk < Koct; kk++)   // ragged octets (log-scale bins)
+                stept(ldt(kk), kk);
+
+            pend = true;
+            pu0 = u0;
+            pu1 = u1;
+            pu2 = u2;
+            pu3 = u3;
+            ppad = uint32_t((A + uint64_t(steps) * kStep) - E);
+            pix = ix;
+        }
         }
     }
+    flush();
+    if (nb)
+        flush_batch();
 }
 
 // ------------------------------------------------------------ k_plan
@@ -1311,9 +1560,9 @@ int launch_binned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_lar
     if (rc)
         return rc;
     Sorted so{c->bins, c->sdesc, c->sidx, c->sinit};
-    uint64_t grid = (d.n + kThreads - 1) / kThreads;
-    if (grid > uint64_t(4 * c->ncu))
-        grid = 4 * c->ncu;
+    uint64_t grid = (d.n + uint64_t(kThreads) * kBinPer - 1) / (uint64_t(kThreads) * kBinPer);
+    if (grid > uint64_t(c->ncu))
+        grid = c->ncu;
     hipLaunchKernelGGL(k_bin_count<kMode>, dim3(grid), dim3(kThreads), 0, s, d, so, skip_large);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(256), 0, s, so);
@@ -1323,7 +1572,8 @@ int launch_binned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_lar
     {
         ScanTimer t(c, s);
         hipLaunchKernelGGL(k_entries_tiny, dim3(c->ncu), dim3(kThreads), 0, s, d, so);
-        hipLaunchKernelGGL(k_entries, dim3(c->ncu), dim3(kThreads), 0, s, d, so);
+        hipLaunchKernelGGL(k_entries<true>, dim3(c->ncu), dim3(kThreads), 0, s, d, so);
+        hipLaunchKernelGGL(k_entries<false>, dim3(c->ncu), dim3(kThreads), 0, s, d, so);
     }
     HIPCHK(hipGetLastError());
     return RAMCRC_OK;
