@@ -638,6 +638,20 @@ struct Sorted {
     uint32_t* init;    // initial state per sorted slot (when the batch has one)
 };
 
+// First window of an entry in k_entries: its 128-byte line, so that every
+// group load is exactly one cache line -- unless the 4 init bytes at S would
+// cross into the second window (S within 3 bytes of the line end); then the
+// 16-byte piece of S, as everywhere else.
+__device__ __forceinline__ uint64_t line_base(uint64_t S)
+{
+    return (S & (kStep - 1)) > kStep - 4 ? (S & ~uint64_t(15)) : (S & ~uint64_t(kStep - 1));
+}
+
+__device__ __forceinline__ uint64_t entry_steps_line(uint64_t S, uint64_t E)
+{
+    return (E - line_base(S) + kStep - 1) / kStep;
+}
+
 __device__ __forceinline__ uint64_t entry_steps(uint64_t S, uint64_t E)
 {
     return (E - (S & ~uint64_t(15)) + kStep - 1) / kStep;
@@ -1103,7 +1117,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_entries(BatchDesc d, Sorted so)
             struct Oct {
                 uint64_t S, E;
                 uint32_t init, ix, steps;
-                u32x4 w[kSmallK];
+                u32x4 w[kSmallK + 1];
             };
             auto load_oct = [&](uint64_t o, Oct& t) {
                 const uint64_t sl = sb + o * kG + g;
@@ -1112,14 +1126,14 @@ __global__ __launch_bounds__(kThreads, 1) void k_entries(BatchDesc d, Sorted so)
                 t.init = d.init ? so.init[sl] : 0xFFFFFFFFu;
                 t.S = (uint64_t(dd.y) << 32) | dd.x;
                 t.E = (uint64_t(dd.w) << 32) | dd.z;
-                t.steps = t.ix != kNoIdx ? K : 0u;
-                const uint64_t A = t.S & ~uint64_t(15);
+                t.steps = t.ix != kNoIdx ? uint32_t(entry_steps_line(t.S, t.E)) : 0u;   // K or K+1
+                const uint64_t A = line_base(t.S);
                 const uint64_t p0 = A + gl * 16;
                 const uint64_t safe = t.steps ? A : dummy;
 #pragma unroll
-                for (int k = 0; k < kSmallK; k++) {
+                for (int k = 0; k <= kSmallK; k++) {
                     const uint64_t a = p0 + uint64_t(k) * kStep;
-                    if (k < int(K))
+                    if (k <= int(K))
                         t.w[k] = load16(t.steps && a < t.E ? a : safe);
                 }
             };
@@ -1128,7 +1142,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_entries(BatchDesc d, Sorted so)
             for (uint64_t o = oa; o < ob; o++) {
                 if (o + 1 < ob)
                     load_oct(o + 1, nxt);
-                const uint64_t A = cur.S & ~uint64_t(15);
+                const uint64_t A = line_base(cur.S);
                 const uint64_t p0 = A + gl * 16;
                 uint32_t u0 = 0, u1 = 0, u2 = 0, u3 = 0;
                 {
@@ -1145,8 +1159,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_entries(BatchDesc d, Sorted so)
                 }
                 const int64_t erel = int64_t(cur.E - p0);
 #pragma unroll
-                for (int k = 1; k < kSmallK; k++) {
-                    if (k < int(K)) {
+                for (int k = 1; k <= kSmallK; k++) {
+                    if (k <= int(K)) {
                         const int64_t de64 = erel - int64_t(k) * int64_t(kStep);
                         const int de = int(de64 < 0 ? 0 : (de64 > 16 ? 16 : de64));
                         u32x4 w = cur.w[k];
@@ -1154,10 +1168,13 @@ __global__ __launch_bounds__(kThreads, 1) void k_entries(BatchDesc d, Sorted so)
                         w.y &= keep_lo(de - 4);
                         w.z &= keep_lo(de - 8);
                         w.w &= keep_lo(de - 12);
-                        u0 = op.apply(lds, u0, w.x);
-                        u1 = op.apply(lds, u1, w.y);
-                        u2 = op.apply(lds, u2, w.z);
-                        u3 = op.apply(lds, u3, w.w);
+                        const bool live = uint32_t(k) < cur.steps;
+                        const uint32_t v0 = op.apply(lds, u0, w.x), v1 = op.apply(lds, u1, w.y);
+                        const uint32_t v2 = op.apply(lds, u2, w.z), v3 = op.apply(lds, u3, w.w);
+                        u0 = live ? v0 : u0;
+                        u1 = live ? v1 : u1;
+                        u2 = live ? v2 : u2;
+                        u3 = live ? v3 : u3;
                     }
                 }
                 pend = true;
@@ -1165,7 +1182,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_entries(BatchDesc d, Sorted so)
                 pu1 = u1;
                 pu2 = u2;
                 pu3 = u3;
-                ppad = uint32_t((A + uint64_t(K) * kStep) - cur.E);
+                ppad = uint32_t((A + uint64_t(cur.steps) * kStep) - cur.E);
                 pix = cur.ix;
                 flush();
                 cur = nxt;
@@ -1186,8 +1203,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_entries(BatchDesc d, Sorted so)
             }
             const uint64_t S = (uint64_t(dd.y) << 32) | dd.x;
             const uint64_t E = (uint64_t(dd.w) << 32) | dd.z;
-            const uint32_t steps = ix != kNoIdx ? uint32_t(entry_steps(S, E)) : 0u;
-            const uint64_t A = S & ~uint64_t(15);
+            const uint32_t steps = ix != kNoIdx ? uint32_t(entry_steps_line(S, E)) : 0u;
+            const uint64_t A = line_base(S);   // windows on 128-byte lines
             const uint64_t p0 = A + gl * 16;
             // longest / shortest entry of the octet (padding slots excluded)
             uint32_t kmax32 = steps, kmin32 = steps ? steps : 0xFFFFFFFFu;
