@@ -84,7 +84,7 @@ struct alignas(16) DeviceTables {
     ramcrc::ByteTable t0;   // X^1 byte step
     uint32_t xblk[4][256];  // x^(8 * 1024 * b * 256^j)
     uint32_t xinv[1024];    // x^(-8 p)
-    uint32_t pos[129][256]; // k_entries_tiny: X^m(byte) for m = 0..128
+    uint32_t pos[132][256]; // k_entries_tiny: row r = X^(r-3)(byte), rows 0..3 (m <= 0) zero
 };
 
 constexpr DeviceTables make_device_tables()
@@ -110,10 +110,10 @@ constexpr DeviceTables make_device_tables()
         t.xinv[p] = acc;
         acc = ramcrc::mulmod(acc, inv8);
     }
-    for (int m = 0; m <= 128; m++) {
+    for (int m = 1; m <= 128; m++) {
         const uint32_t c = ramcrc::xpow8(uint64_t(m));
         for (uint32_t b = 0; b < 256; b++)
-            t.pos[m][b] = ramcrc::mulmod(b, c);
+            t.pos[m + 3][b] = ramcrc::mulmod(b, c);
     }
     return t;
 }
@@ -619,7 +619,9 @@ constexpr int kPU = 4;                     // ping-pong depth (pipelined bins)
 constexpr uint32_t kNoIdx = 0xFFFFFFFFu;   // empty slot
 constexpr uint64_t kOctetCost = 4;         // per-octet overhead in step units (work split)
 constexpr int kBinPer = 4;                 // entries per thread per tile (count/scatter)
-constexpr uint32_t kLdsTiny = 129 * 1024;  // k_entries_tiny: X^m(byte), m = 0..128
+
+constexpr uint32_t kTinyRow0 = 3;            // k_entries_tiny: row of distance m is m + 3
+constexpr uint32_t kLdsTiny = 132 * 1024;    // k_entries_tiny: X^m(byte), m = -3..128
 
 struct BinTable {
     uint64_t start[kNB];      // first sorted slot of the bin (multiple of 8)
@@ -936,17 +938,28 @@ __device__ __forceinline__ uint32_t keep_lo(int c)
     return c >= 4 ? 0xFFFFFFFFu : (1u << (8 * c)) - 1u;
 }
 
+// XOR of the 8 lanes of each lane group, valid in lanes 0-3 of the group
+// (DPP: quad swaps, then the other quad of the 16-lane row; no LDS traffic).
+__device__ __forceinline__ uint32_t group8_xor(uint32_t v)
+{
+    v ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0xB1, 0xF, 0xF, false));   // quad_perm 1,0,3,2
+    v ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x4E, 0xF, 0xF, false));   // quad_perm 2,3,0,1
+    v ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x12C, 0xF, 0xF, false));  // row_ror:12 (lane + 4)
+    return v;
+}
+
 // Entries of at most one 128-byte window (bins 0-1; 100-byte log entries are
 // here): no Horner step and no per-entry multiply.  Byte b at distance m from
-// the entry end contributes X^m(b), read from a 129 x 256 LDS table, so a lane
-// does 16 lookups for its 16 bytes and the group XORs its 8 lanes.  Eight
-// octets (64 entries, one descriptor per lane) share one load round.
+// the entry end contributes X^m(b), read from a 132 x 256 LDS table (rows for
+// m <= 0 are zero), so a lane does 16 lookups for its 16 bytes and the group
+// XORs its 8 lanes.  Every lane reads its group's descriptor itself (8 lanes,
+// one address: no cross-lane shuffles), and eight octets share one load round.
 __global__ __launch_bounds__(kThreads, 1) void k_entries_tiny(BatchDesc d, Sorted so)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsTiny];
     if (so.bt->start[2] == so.bt->start[0])
         return;   // no entry of at most one window (uniform: every wave exits)
-    fill_plain(lds, 0, &g_tab.pos[0][0], 129 * 256);
+    fill_plain(lds, 0, &g_tab.pos[0][0], 132 * 256);
     __syncthreads();
     const uint32_t* tab = reinterpret_cast<const uint32_t*>(lds);
 
@@ -961,61 +974,73 @@ __global__ __launch_bounds__(kThreads, 1) void k_entries_tiny(BatchDesc d, Sorte
     const uint64_t dummy = reinterpret_cast<uint64_t>(so.bt);
 
     for (uint64_t r = wave; r < rounds; r += nwaves) {
-        const uint64_t slot = s0 + r * 64 + lane;
-        u32x4 dd = {0u, 0u, 0u, 0u};
-        uint32_t didx = kNoIdx, dinit = 0xFFFFFFFFu;
-        if (slot < s1) {
-            dd = so.desc[slot];
-            didx = so.idx[slot];
-            if (d.init)
-                dinit = so.init[slot];
-        }
-        const uint64_t dS = (uint64_t(dd.y) << 32) | dd.x;
-        const uint64_t dE = (uint64_t(dd.w) << 32) | dd.z;
+        uint32_t geo[8], ix[8], init[8];
         u32x4 w[8];
 #pragma unroll
         for (int q = 0; q < 8; q++) {
-            const uint64_t S = shfl64(dS, q * kG + g), E = shfl64(dE, q * kG + g);
+            const uint64_t slot = s0 + r * 64 + q * kG + g;
+            u32x4 dd = {0u, 0u, 0u, 0u};
+            ix[q] = kNoIdx;
+            init[q] = 0xFFFFFFFFu;
+            if (slot < s1) {
+                dd = so.desc[slot];
+                ix[q] = so.idx[slot];
+                if (d.init)
+                    init[q] = so.init[slot];
+            }
+            const uint64_t S = (uint64_t(dd.y) << 32) | dd.x;
+            const uint64_t E = (uint64_t(dd.w) << 32) | dd.z;
             const uint64_t A = S & ~uint64_t(15);
             const uint64_t a = A + gl * 16;
+            // geo: len (bits 0-7, < 256), S - a + 128 (8-15), E - a + 128 (16-23)
+            geo[q] = uint32_t(E - S) | (uint32_t(int(int64_t(S - a)) + 128) << 8) |
+                     (uint32_t(int(int64_t(E - a)) + 128) << 16);
             const bool big = E - S >= 4;
             const bool ok = big && a < E;
-            const u32x4 v = load16(ok ? a : (big ? A : dummy));
-            w[q] = ok ? v : u32x4{0u, 0u, 0u, 0u};
+            w[q] = load16(ok ? a : (big ? A : dummy));   // pieces past E hit zero rows
         }
 #pragma unroll
         for (int q = 0; q < 8; q++) {
-            const int src = q * kG + g;
-            const uint64_t S = shfl64(dS, src), E = shfl64(dE, src);
-            const uint32_t init = __shfl(dinit, src, kWaveSize);
-            const uint64_t a = (S & ~uint64_t(15)) + gl * 16;
+            const uint32_t len = geo[q] & 0xFF;
+            const int ds = int((geo[q] >> 8) & 0xFF) - 128;    // S - a (<= 15)
+            const int e = int((geo[q] >> 16) & 0xFF) - 128;    // E - a (<= 128)
             uint32_t R = 0;
-            if (E - S >= 4) {
-                const u32x4 x = fix_piece(w[q], a, S, E, init);
-                // table row m = distance of the byte from E; bytes at or past E
-                // are zero and clamp to row 128 (X^128(0) = 0)
-                const uint32_t e10 = uint32_t(E - a) << 10;
-                const uint32_t ws[4] = {x.x, x.y, x.z, x.w};
+            if (len >= 4) {
+                // Byte at distance m from E contributes row m + 3; bytes at or
+                // past E (m <= 0) land in the zero rows, so only the bytes
+                // before S need a mask.  The init is not injected into the
+                // data: its byte k sits at distance len - k (4 more lookups).
+                const uint32_t ws[4] = {w[q].x, w[q].y, w[q].z, w[q].w};
+                uint32_t v[16];
 #pragma unroll
-                for (int j = 0; j < 4; j++)
+                for (int j = 0; j < 4; j++) {
+                    const uint32_t x = ws[j] & ~keep_lo(ds - 4 * j);
+                    const uint32_t base = uint32_t(max(e - 4 * j, 0)) << 8;   // row of byte 0, - 3
 #pragma unroll
-                    for (int t = 0; t < 4; t++) {
-                        const uint32_t c = uint32_t(4 * j + t) << 10;
-                        const uint32_t row = min(e10 - c, 128u << 10);
-                        const uint32_t byte = (ws[j] >> (8 * t)) & 0xFF;
-                        R ^= tab[(row | (byte << 2)) >> 2];
-                    }
+                    for (int t = 0; t < 4; t++)
+                        v[4 * j + t] = tab[base + ((x >> (8 * t)) & 0xFF) + (kTinyRow0 - t) * 256];
+                }
+                const uint32_t in = init[q];
+                const uint32_t ib = (len + kTinyRow0) << 8;
+                const uint32_t i0 = tab[ib + (in & 0xFF)], i1 = tab[ib - 256 + ((in >> 8) & 0xFF)];
+                const uint32_t i2 = tab[ib - 512 + ((in >> 16) & 0xFF)], i3 = tab[ib - 768 + (in >> 24)];
+                // one wait for all 20 lookups, then a 3-input XOR tree
+                const uint32_t ri = gl == 0 ? xor3(i0, i1, i2) ^ i3 : 0u;
+                const uint32_t t0 = xor3(v[0], v[1], v[2]), t1 = xor3(v[3], v[4], v[5]);
+                const uint32_t t2 = xor3(v[6], v[7], v[8]), t3 = xor3(v[9], v[10], v[11]);
+                const uint32_t t4 = xor3(v[12], v[13], v[14]), t5 = xor3(v[15], ri, t0);
+                R = xor3(xor3(t1, t2, t3), t4, t5);
             } else if (gl == 0) {
-                R = init;
-                for (uint64_t p = S; p < E; p++)
-                    R = tab[256 + ((R ^ *(const gu8*)p) & 0xFF)] ^ (R >> 8);
+                // 0-3 bytes: byte steps from the initial state
+                R = init[q];
+                const u32x4 dd = so.desc[s0 + r * 64 + q * kG + g];   // rare: reload S
+                const uint64_t S = (uint64_t(dd.y) << 32) | dd.x;
+                for (uint32_t k = 0; k < len; k++)
+                    R = tab[(1 + kTinyRow0) * 256 + ((R ^ *(const gu8*)(S + k)) & 0xFF)] ^ (R >> 8);
             }
-            R ^= __shfl_xor(R, 1, kWaveSize);
-            R ^= __shfl_xor(R, 2, kWaveSize);
-            R ^= __shfl_xor(R, 4, kWaveSize);
-            const uint32_t ix = __shfl(didx, src, kWaveSize);
-            if (gl == 0 && ix != kNoIdx)
-                d.out[ix] = finalize ? ~R : R;
+            R = group8_xor(R);
+            if (gl == 0 && ix[q] != kNoIdx)
+                d.out[ix[q]] = finalize ? ~R : R;
         }
     }
 }
