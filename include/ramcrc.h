@@ -122,6 +122,88 @@ int ramcrc_batch_host(ramcrc_ctx* ctx, const void* const* ptrs, const uint64_t* 
 int ramcrc_stream_host(ramcrc_ctx* ctx, const void* h_base, uint64_t seg_bytes,
                        uint64_t nseg, uint32_t* h_out, uint32_t flags, int batch, int depth);
 
+/* ------------------------------------------- recovery-segment verify --- */
+
+/* SegmentCertificate (src/LogMetadata.h:85-128): 8 bytes, packed. */
+typedef struct ramcrc_seg_cert {
+    uint32_t segment_length;
+    uint32_t checksum;
+} ramcrc_seg_cert;
+
+/* One walked log entry (src/Segment.h:99-195): `offset` is the entry's
+ * EntryHeader byte within its segment, `header` that byte (type = header &
+ * 0x3f, length bytes = ((header >> 6) & 3) + 1) plus RAMCRC_SEG_ENTRY_OVERLONG
+ * when the payload would run past the segment capacity (reachable only
+ * through the uint32_t offset wrap of the reference's walk), `length` the
+ * payload length; the payload starts at offset + 1 + length bytes. */
+#define RAMCRC_SEG_ENTRY_OVERLONG 0x100u
+typedef struct ramcrc_seg_entry {
+    uint32_t segment;
+    uint32_t offset;
+    uint32_t length;
+    uint32_t header;
+} ramcrc_seg_entry;
+
+/* Per-segment result of the walk (and of the object verify). */
+typedef struct ramcrc_seg_status {
+    uint32_t flags;        /* RAMCRC_SEG_* */
+    uint32_t checksum;     /* metadata checksum the walk computed (over the entries walked + length) */
+    uint32_t entries;      /* entries walked */
+    uint32_t bad_objects;  /* objects whose Object::Header::checksum did not match */
+} ramcrc_seg_status;
+
+#define RAMCRC_SEG_OK 1u              /* Segment::checkMetadataIntegrity returned true */
+#define RAMCRC_SEG_PAST_CAPACITY 2u   /* an entry ran past the segment capacity (src/Segment.cc:777-783) */
+#define RAMCRC_SEG_PAST_LENGTH 4u     /* entries ran past certificate.segmentLength (:786-790) */
+#define RAMCRC_SEG_BAD_CHECKSUM 8u    /* certificate checksum mismatch (:795-797) */
+#define RAMCRC_SEG_TABLE_FULL 16u     /* entry table capacity exhausted: records dropped */
+#define RAMCRC_SEG_CYCLE 32u          /* the walk revisited an offset (uint32_t wrap): the
+                                         reference's loop would not terminate; stopped */
+#define RAMCRC_LOG_ENTRY_TYPE_OBJ 2u  /* LOG_ENTRY_TYPE_OBJ, src/LogEntryTypes.h:35 */
+
+/* Segment::checkMetadataIntegrity (src/Segment.cc:758-800) for n_seg segments
+ * at d_base + i*seg_stride, each of seg_capacity bytes (a multiple of 16; the
+ * reference's segletBlocks.size() * segletSize), against d_certs[i].  One
+ * wavefront walks each segment's length-prefixed entries.  Writes
+ * d_status[i] and appends one ramcrc_seg_entry per complete entry to
+ * d_entries (up to entries_cap; the order across segments is unspecified,
+ * within a segment it is increasing).  *d_n_entries (device) receives the
+ * number of entries walked (may exceed entries_cap: see TABLE_FULL).
+ * d_base 16-byte aligned, seg_stride a multiple of 16.  Stream-ordered. */
+int ramcrc_segment_walk_device(ramcrc_ctx* ctx, const void* d_base, uint64_t seg_stride,
+                               uint32_t seg_capacity, uint64_t n_seg,
+                               const ramcrc_seg_cert* d_certs, ramcrc_seg_status* d_status,
+                               ramcrc_seg_entry* d_entries, uint64_t entries_cap,
+                               uint64_t* d_n_entries, void* stream);
+
+/* Object::computeChecksum (src/Object.cc:805-819) for every LOG_ENTRY_TYPE_OBJ
+ * record of a walk whose segment passed the metadata check (d_status flags
+ * RAMCRC_SEG_OK; records of failed segments are skipped, as
+ * RecoverySegmentBuilder::build stops there), compared with the object's
+ * stored checksum as ObjectManager::replaySegment does
+ * (src/ObjectManager.cc:659-669): CRC32C over payload bytes [4, length) into
+ * d_obj_crc[i] (other records: not written), and
+ * d_status[segment].bad_objects += 1 per mismatch (objects shorter than their
+ * 24-byte header or flagged OVERLONG count as mismatches).  Objects of
+ * >= 64 KiB are scanned by all CUs, smaller ones by the small-entry kernels.
+ * Stream-ordered after the walk that produced the table. */
+int ramcrc_verify_objects_device(ramcrc_ctx* ctx, const void* d_base, uint64_t seg_stride,
+                                 const ramcrc_seg_entry* d_entries, uint64_t entries_cap,
+                                 const uint64_t* d_n_entries, uint32_t* d_obj_crc,
+                                 ramcrc_seg_status* d_status, void* stream);
+
+/* Host append path (src/Segment.cc:197-228 with src/Object.cc:213-218):
+ * appends LOG_ENTRY_TYPE_OBJ entries holding objects {tableId 0, key = 8-byte
+ * counter from first_key, version 0, timestamp 0, value_len value bytes} to an
+ * empty segment of `capacity` bytes until the next one does not fit, as
+ * RecoverSegmentBenchmark::run fills its segments
+ * (nanobenchmarks/RecoverSegmentBenchmark.cc:131-146).  The value bytes are
+ * whatever `seg` already holds at their positions; bytes after the last entry
+ * are zeroed.  Writes the certificate (Segment::getAppendedLength,
+ * src/Segment.cc:672-684) and the object count. */
+int ramcrc_segment_fill_objects(uint8_t* seg, uint32_t capacity, uint32_t value_len,
+                                uint64_t first_key, uint32_t* n_objects, ramcrc_seg_cert* cert);
+
 /* Kernel timing (for benchmarks): when enabled, every launch brackets its
  * byte-scan kernel (k_chunks, or k_entries on the small path) with HIP events
  * on the launch stream.  ramcrc_ctx_scan_time waits for the recorded events,

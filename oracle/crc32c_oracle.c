@@ -282,3 +282,160 @@ int oracle_segments_mt(const uint8_t* base, uint64_t seg_bytes, uint64_t nseg,
         pthread_join(th[t], NULL);
     return 0;
 }
+
+/* ------------------------------------------------------------------------
+ * Segments and objects.  Restated from:
+ *   - Segment::append (src/Segment.cc:197-228) and hasSpaceFor (:136-154):
+ *     |EntryHeader (type | (lengthBytes-1) << 6)|length, 1-4 B LE|payload|,
+ *     EntryHeader(type, length) picking lengthBytes (src/Segment.h:131-150);
+ *     the segment's running Crc32C over each header byte and length bytes;
+ *   - Segment::getAppendedLength (src/Segment.cc:672-684): certificate =
+ *     {head, getResult() after also covering head (4 B LE)};
+ *   - Segment::checkMetadataIntegrity (src/Segment.cc:758-800), including its
+ *     uint32_t offset arithmetic and the order of its three failure checks;
+ *   - Object::assembleForLog / computeChecksum (src/Object.cc:213-218,
+ *     :805-819): Crc32C over the serialized object minus its first 4 bytes;
+ *     Object(key, value, ...) key layout (src/Object.cc:107-141);
+ *   - RecoverSegmentBenchmark::run's fill (nanobenchmarks/
+ *     RecoverSegmentBenchmark.cc:131-146): tableId 0, 8-byte counter keys,
+ *     version 0, timestamp 0.
+ * Flags: 1 OK, 2 past capacity, 4 past certificate length, 8 bad checksum,
+ * 16 entry table full, 32 cyclic walk (the product's RAMCRC_SEG_* values).
+ * ---------------------------------------------------------------------- */
+static uint32_t oracle_u32le(const uint8_t* p)
+{
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+uint32_t oracle_build_object_segment(uint8_t* seg, uint32_t capacity, uint32_t value_len,
+                                     uint64_t first_key, uint32_t* cert_len, uint32_t* cert_crc)
+{
+    uint32_t objlen = 24u + 1u + 2u + 8u + value_len;
+    uint32_t lb = objlen < 0x100u ? 1 : objlen < 0x10000u ? 2 : objlen < 0x1000000u ? 3 : 4;
+    uint32_t head = 0, n = 0, meta = 0xFFFFFFFFu;
+    uint64_t key = first_key;
+    for (;;) {
+        uint32_t need = 1 + lb + objlen;
+        uint32_t left = capacity - head;
+        if (need > left)
+            break;
+        uint8_t* e = seg + head;
+        uint8_t hb = (uint8_t)(2u | ((lb - 1) << 6));   /* LOG_ENTRY_TYPE_OBJ */
+        e[0] = hb;
+        meta = oracle_slicing8(meta, &hb, 1);
+        uint8_t lenle[4] = {(uint8_t)objlen, (uint8_t)(objlen >> 8), (uint8_t)(objlen >> 16),
+                            (uint8_t)(objlen >> 24)};
+        memcpy(e + 1, lenle, lb);
+        meta = oracle_slicing8(meta, lenle, lb);
+        uint8_t* o = e + 1 + lb;
+        memset(o, 0, 24);
+        o[24] = 1;
+        o[25] = 8;
+        o[26] = 0;
+        for (int k = 0; k < 8; k++)
+            o[27 + k] = (uint8_t)(key >> (8 * k));
+        uint32_t ck = ~oracle_slicing8(0xFFFFFFFFu, o + 4, objlen - 4);
+        for (int k = 0; k < 4; k++)
+            o[k] = (uint8_t)(ck >> (8 * k));
+        head += need;
+        n++;
+        key++;
+    }
+    memset(seg + head, 0, capacity - head);
+    uint8_t hl[4] = {(uint8_t)head, (uint8_t)(head >> 8), (uint8_t)(head >> 16), (uint8_t)(head >> 24)};
+    *cert_len = head;
+    *cert_crc = ~oracle_slicing8(meta, hl, 4);
+    return n;
+}
+
+/* table: 4 uint32 per entry {segment, offset, length, header}; returns flags. */
+uint32_t oracle_check_metadata(const uint8_t* seg, uint64_t capacity, uint32_t cert_len,
+                               uint32_t cert_crc, uint32_t segment, uint32_t* checksum_out,
+                               uint32_t* n_out, uint32_t* table, uint64_t table_cap)
+{
+    uint32_t offset = 0, crc = 0xFFFFFFFFu, n = 0, flags = 0;
+    uint64_t steps = 0;
+    while (offset < cert_len && (uint64_t)offset < capacity) {
+        /* The walk is deterministic in `offset` and stays below the capacity,
+         * so more than `capacity` steps means a position repeated: through the
+         * uint32_t wrap the reference's loop would never end.  Stop (flag 32). */
+        if (++steps > capacity) {
+            flags |= 32;
+            break;
+        }
+        uint8_t hdr = seg[offset];
+        crc = oracle_slicing8(crc, &hdr, 1);
+        uint32_t lb = (uint32_t)(hdr >> 6) + 1;
+        uint8_t lenle[4] = {0, 0, 0, 0};
+        for (uint32_t k = 0; k < lb; k++)   /* copyOut: bytes past the capacity stay 0 */
+            if ((uint64_t)offset + 1 + k < capacity)
+                lenle[k] = seg[offset + 1 + k];
+        uint32_t length = oracle_u32le(lenle);
+        crc = oracle_slicing8(crc, lenle, lb);
+        uint32_t next = offset + 1 + lb + length;   /* uint32_t, as the reference */
+        if ((uint64_t)next > capacity) {
+            flags |= 2;
+            break;
+        }
+        if (table && n < table_cap) {
+            /* 0x100: the payload runs past the capacity (only reachable through
+             * the uint32_t wrap of `offset`); such an object cannot be read */
+            uint64_t end = (uint64_t)offset + 1 + lb + length;
+            table[4 * (uint64_t)n + 0] = segment;
+            table[4 * (uint64_t)n + 1] = offset;
+            table[4 * (uint64_t)n + 2] = length;
+            table[4 * (uint64_t)n + 3] = hdr | (end > capacity ? 0x100u : 0u);
+        }
+        n++;
+        offset = next;
+    }
+    uint8_t cl[4] = {(uint8_t)cert_len, (uint8_t)(cert_len >> 8), (uint8_t)(cert_len >> 16),
+                     (uint8_t)(cert_len >> 24)};
+    uint32_t fin = ~oracle_slicing8(crc, cl, 4);
+    if (!(flags & (2 | 32))) {
+        if (offset > cert_len)
+            flags |= 4;
+        else
+            flags |= fin == cert_crc ? 1 : 8;
+    }
+    if (table && n > table_cap)
+        flags |= 16;
+    if (checksum_out)
+        *checksum_out = fin;
+    if (n_out)
+        *n_out = n;
+    return flags;
+}
+
+/* Object::computeChecksum of every OBJ record (4 uint32 each) of segments at
+ * base + segment*stride whose metadata check passed (seg_ok[segment] != 0, or
+ * every segment when seg_ok is NULL) -- RecoverySegmentBuilder::build stops at
+ * a failed check (src/RecoverySegmentBuilder.cc:61-203), so nothing of such a
+ * segment is replayed.  crc_out[i] for readable objects of >= 24 bytes;
+ * returns the number of mismatches (short or unreadable objects count as
+ * mismatches) and adds them to bad_per_seg[segment] when that is non-NULL. */
+uint64_t oracle_verify_objects(const uint8_t* base, uint64_t stride, const uint32_t* table,
+                               uint64_t n, const uint8_t* seg_ok, uint32_t* crc_out,
+                               uint32_t* bad_per_seg)
+{
+    uint64_t bad = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        const uint32_t* r = table + 4 * i;
+        if ((r[3] & 0x3f) != 2 || (seg_ok && !seg_ok[r[0]]))
+            continue;
+        int ok = 0;
+        if (r[2] >= 24 && !(r[3] & 0x100)) {
+            const uint8_t* payload = base + (uint64_t)r[0] * stride + r[1] + 1 + ((r[3] >> 6) & 3) + 1;
+            uint32_t c = ~oracle_slicing8(0xFFFFFFFFu, payload + 4, r[2] - 4);
+            if (crc_out)
+                crc_out[i] = c;
+            ok = c == oracle_u32le(payload);
+        }
+        if (!ok) {
+            bad++;
+            if (bad_per_seg)
+                bad_per_seg[r[0]]++;
+        }
+    }
+    return bad;
+}

@@ -57,6 +57,17 @@ def lib():
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                      ctypes.c_int, ctypes.c_int]
         L.oracle_segments_mt.restype = ctypes.c_int
+        L.oracle_build_object_segment.restype = ctypes.c_uint32
+        L.oracle_build_object_segment.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_check_metadata.restype = ctypes.c_uint32
+        L.oracle_check_metadata.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+        L.oracle_verify_objects.restype = ctypes.c_uint64
+        L.oracle_verify_objects.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                            ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p]
         L.oracle_segments_mt.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.oracle_have_sse42.restype = ctypes.c_int
@@ -157,3 +168,46 @@ def segments(base, seg_bytes, nseg, threads=1, impl=IMPL_SSE42, pin=True, use_re
     if rc != 0:
         raise RuntimeError("thread start failed")
     return out
+
+
+# ---------------------------------------------------------------- segments
+def build_object_segment(seg, value_len, first_key=0):
+    """Restated RecoverSegmentBenchmark fill of `seg` (numpy uint8, value bytes
+    pre-filled); returns (n_objects, segment_length, checksum)."""
+    cl = np.zeros(1, np.uint32)
+    cc = np.zeros(1, np.uint32)
+    n = lib().oracle_build_object_segment(_ptr(seg), seg.size, value_len, first_key,
+                                          _ptr(cl), _ptr(cc))
+    return int(n), int(cl[0]), int(cc[0])
+
+
+def check_metadata(seg, cert_len, cert_crc, segment=0, capacity=None, table_cap=None):
+    """Restated Segment::checkMetadataIntegrity.  Returns (flags, checksum,
+    n_entries, table uint32[n, 4])."""
+    seg = np.ascontiguousarray(seg, dtype=np.uint8)
+    capacity = seg.size if capacity is None else capacity
+    cap = (capacity // 2 + 1) if table_cap is None else table_cap
+    table = np.zeros((max(cap, 1), 4), np.uint32)
+    ck = np.zeros(1, np.uint32)
+    n = np.zeros(1, np.uint32)
+    flags = lib().oracle_check_metadata(_ptr(seg), capacity, cert_len & 0xFFFFFFFF,
+                                        cert_crc & 0xFFFFFFFF, segment, _ptr(ck), _ptr(n),
+                                        _ptr(table), cap)
+    k = min(int(n[0]), cap)
+    return int(flags), int(ck[0]), int(n[0]), table[:k].copy()
+
+
+def verify_objects(base, stride, table, nseg=None, seg_ok=None):
+    """Restated Object::computeChecksum comparison over walk records of the
+    segments whose metadata check passed (seg_ok: bool[nseg], None = all).
+    Returns (bad_total, crc uint32[n], bad_per_segment uint32[nseg])."""
+    base = np.ascontiguousarray(base, dtype=np.uint8)
+    table = np.ascontiguousarray(table, dtype=np.uint32).reshape(-1, 4)
+    n = table.shape[0]
+    crc = np.zeros(max(n, 1), np.uint32)
+    nseg = (int(table[:, 0].max()) + 1 if n else 1) if nseg is None else nseg
+    bad = np.zeros(max(nseg, 1), np.uint32)
+    ok = None if seg_ok is None else np.ascontiguousarray(seg_ok, dtype=np.uint8)
+    total = lib().oracle_verify_objects(_ptr(base), stride, _ptr(table), n,
+                                        None if ok is None else _ptr(ok), _ptr(crc), _ptr(bad))
+    return int(total), crc[:n], bad[:nseg]

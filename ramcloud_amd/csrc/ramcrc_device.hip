@@ -323,12 +323,15 @@ struct BatchDesc {
     const uint8_t* base;     // d_base
     const uint64_t* off;     // general mode
     const uint64_t* len;     // general mode
-    uint64_t seg_bytes;      // uniform mode
-    uint64_t n;              // buffers
+    uint64_t seg_bytes;      // uniform mode; segment stride in record mode
+    uint64_t n;              // buffers (record mode: table capacity)
     const uint32_t* init;    // nullable
     uint32_t* out;
     uint32_t flags;
     uint32_t cshift;         // log2 chunk bytes of this launch (k_chunks/k_combine)
+    const u32x4* rec;        // record mode: ramcrc_seg_entry table
+    const uint64_t* n_dev;   // record mode: live entry count (device), <= n
+    const u32x4* seg_status; // record mode: ramcrc_seg_status per segment (walk result)
 };
 
 // Buffer addressing modes.
@@ -336,19 +339,50 @@ struct BatchDesc {
 //                of the chunk size -> chunk g maps to (g / per, g % per).
 //   kSegUniform: same geometry, any alignment -> goes through the plan.
 //   kTable:      buffer i = base + off[i], len[i] -> goes through the plan.
-enum Mode { kSegAligned = 0, kSegUniform = 1, kTable = 2 };
+//   kRecords:    buffer i = the object of segment-walk record i: bytes
+//                [4, length) of its payload (Object::computeChecksum,
+//                src/Object.cc:805-819).  Inactive: records that are not
+//                objects, objects shorter than their header or running past
+//                the segment (kRecOverlong), and every record of a segment
+//                whose metadata check failed (RecoverySegmentBuilder::build
+//                stops there, src/RecoverySegmentBuilder.cc:61-203).
+enum Mode { kSegAligned = 0, kSegUniform = 1, kTable = 2, kRecords = 3 };
+
+constexpr uint32_t kObjHeaderBytes = 24;   // Object::Header, src/Object.h:137-182
+constexpr uint32_t kRecOverlong = 0x100;   // record header bit: payload past the capacity
 
 template <int kMode>
-__device__ __forceinline__ void buffer_range(const BatchDesc& d, uint64_t i, uint64_t& S,
+__device__ __forceinline__ uint64_t entry_count(const BatchDesc& d)
+{
+    if (kMode == kRecords) {
+        const uint64_t live = *d.n_dev;
+        return live < d.n ? live : d.n;
+    }
+    return d.n;
+}
+
+// [S, E) of buffer i; false for an inactive record (then S == E).
+template <int kMode>
+__device__ __forceinline__ bool buffer_range(const BatchDesc& d, uint64_t i, uint64_t& S,
                                              uint64_t& E)
 {
-    if (kMode != kTable) {
+    if (kMode == kRecords) {
+        const u32x4 r = d.rec[i];   // {segment, offset, length, header}
+        const uint64_t payload = reinterpret_cast<uint64_t>(d.base) + uint64_t(r.x) * d.seg_bytes +
+                                 r.y + 1 + ((r.w >> 6) & 3) + 1;
+        const bool obj = (r.w & (0x3f | kRecOverlong)) == RAMCRC_LOG_ENTRY_TYPE_OBJ &&
+                         r.z >= kObjHeaderBytes && (d.seg_status[r.x].x & RAMCRC_SEG_OK);
+        S = payload + 4;
+        E = obj ? payload + r.z : S;
+        return obj;
+    } else if (kMode != kTable) {
         S = reinterpret_cast<uint64_t>(d.base) + i * d.seg_bytes;
         E = S + d.seg_bytes;
     } else {
         S = reinterpret_cast<uint64_t>(d.base) + d.off[i];
         E = S + d.len[i];
     }
+    return true;
 }
 
 __device__ __forceinline__ uint64_t chunk_count(uint64_t S, uint64_t E, uint32_t cshift)
@@ -568,12 +602,12 @@ __global__ __launch_bounds__(256) void k_combine(BatchDesc d, Plan pl, uint64_t 
     const uint64_t i = uint64_t(blockIdx.x) * (256 / kWaveSize) + threadIdx.x / kWaveSize;
     if (blockIdx.x == 0 && threadIdx.x == 0)
         *pl.ticket = 0;   // k_chunks of this launch is complete (same stream)
-    if (i >= d.n)
+    if (i >= entry_count<kMode>(d))
         return;
     uint64_t S, E;
     buffer_range<kMode>(d, i, S, E);
     if (!is_large(E - S))
-        return;   // handled by k_entries
+        return;   // handled by k_entries (or inactive)
     if (kMode != kSegAligned && ((*pl.status) & 1u))
         return;   // k_chunks refused the launch (partials overflow)
     const uint64_t g0 = kMode == kSegAligned ? i * per_seg
@@ -715,19 +749,19 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
         h[t] = kmx[t] = 0;
     __syncthreads();
     const uint64_t tile = uint64_t(blockDim.x) * kBinPer;
-    for (uint64_t base = uint64_t(blockIdx.x) * tile; base < d.n; base += uint64_t(gridDim.x) * tile) {
+    const uint64_t n = entry_count<kMode>(d);
+    for (uint64_t base = uint64_t(blockIdx.x) * tile; base < n; base += uint64_t(gridDim.x) * tile) {
         uint64_t S[kBinPer], E[kBinPer];
+        bool act[kBinPer];
 #pragma unroll
         for (int q = 0; q < kBinPer; q++) {   // all loads first
             const uint64_t i = base + uint64_t(q) * blockDim.x + threadIdx.x;
             S[q] = E[q] = 0;
-            if (i < d.n)
-                buffer_range<kMode>(d, i, S[q], E[q]);
+            act[q] = i < n && buffer_range<kMode>(d, i, S[q], E[q]);
         }
 #pragma unroll
         for (int q = 0; q < kBinPer; q++) {
-            const uint64_t i = base + uint64_t(q) * blockDim.x + threadIdx.x;
-            const bool active = i < d.n && !(skip_large && is_large(E[q] - S[q]));
+            const bool active = act[q] && !(skip_large && is_large(E[q] - S[q]));
             const int b = active ? bin_of(S[q], E[q]) : 0;
             if (active && b > 32)
                 atomicMax(&kmx[b], uint32_t(entry_steps(S[q], E[q])));
@@ -817,21 +851,21 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter(BatchDesc d, Sorted so
         cnt[t] = 0;
     __syncthreads();
     const uint64_t tile = uint64_t(blockDim.x) * kBinPer;
-    for (uint64_t t0 = uint64_t(blockIdx.x) * tile; t0 < d.n; t0 += uint64_t(gridDim.x) * tile) {
+    const uint64_t n = entry_count<kMode>(d);
+    for (uint64_t t0 = uint64_t(blockIdx.x) * tile; t0 < n; t0 += uint64_t(gridDim.x) * tile) {
         uint64_t S[kBinPer], E[kBinPer];
         int b[kBinPer];
         uint32_t lp[kBinPer];
+        bool act[kBinPer];
 #pragma unroll
         for (int q = 0; q < kBinPer; q++) {
             const uint64_t i = t0 + uint64_t(q) * blockDim.x + threadIdx.x;
             S[q] = E[q] = 0;
-            if (i < d.n)
-                buffer_range<kMode>(d, i, S[q], E[q]);
+            act[q] = i < n && buffer_range<kMode>(d, i, S[q], E[q]);
         }
 #pragma unroll
         for (int q = 0; q < kBinPer; q++) {
-            const uint64_t i = t0 + uint64_t(q) * blockDim.x + threadIdx.x;
-            const bool active = i < d.n && !(skip_large && is_large(E[q] - S[q]));
+            const bool active = act[q] && !(skip_large && is_large(E[q] - S[q]));
             b[q] = active ? bin_of(S[q], E[q]) : 0;
             uint32_t wbase;
             const uint32_t rank = wave_bin_add(cnt, b[q], active, wbase);
@@ -1354,7 +1388,7 @@ __global__ __launch_bounds__(kThreads) void k_plan_count(BatchDesc d, Plan pl)
     __shared__ uint64_t wsum[kWavesPerGroup];
     const uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
     uint64_t c = 0;
-    if (i < d.n) {
+    if (i < entry_count<kMode>(d)) {   // local[] is still written for every i < d.n
         uint64_t S, E;
         buffer_range<kMode>(d, i, S, E);
         c = is_large(E - S) ? chunk_count(S, E, d.cshift) : 0;
@@ -1638,6 +1672,168 @@ int launch_planned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s)
     hipLaunchKernelGGL(k_combine<kMode>, dim3((d.n + 3) / 4), dim3(256), 0, s, d, pl, uint64_t(0));
     HIPCHK(hipGetLastError());
     return launch_binned<kMode>(c, d, s, 1);
+}
+
+// ------------------------------------------------------------ segment walk
+// Segment::checkMetadataIntegrity (src/Segment.cc:758-800) on the device: one
+// wavefront per segment.  The walk is a pointer chase through length-prefixed
+// entries (|EntryHeader|length 1-4 B|payload|, src/Segment.h:99-112), so it is
+// latency-bound, not bandwidth-bound: the wave stages a 16 KiB window of the
+// segment in LDS around the current entry header (coalesced loads), and the
+// chase runs on LDS reads; an entry larger than the window makes the next
+// window start at the next header, so payload bytes are never fetched.  The
+// metadata checksum (header byte + length bytes of every entry, then the
+// certificate length) is updated with <= 4-byte slicing steps from LDS tables.
+// Complete entries are appended to the record table 64 at a time (one atomic
+// per 64 records).
+constexpr uint32_t kWalkWin = 16384;
+
+struct WalkDesc {
+    const uint8_t* base;
+    uint64_t stride;
+    uint64_t capacity;
+    uint64_t nseg;
+    const ramcrc_seg_cert* certs;
+    ramcrc_seg_status* status;
+    u32x4* entries;
+    uint64_t cap;
+    unsigned long long* n_entries;
+};
+
+// CRC32C update by the m (1..4) bytes in the low end of v; t[j][b] = X^(j+1)(b).
+__device__ __forceinline__ uint32_t crc_small(const uint32_t* t, uint32_t c, uint32_t v, uint32_t m)
+{
+    const uint32_t x = c ^ v;
+    uint32_t r = m >= 4 ? 0u : (c >> (8 * m));
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++)
+        if (k < m)
+            r ^= t[(m - 1 - k) * 256 + ((x >> (8 * k)) & 0xFF)];
+    return r;
+}
+
+__global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t win[kWalkWin + 16];
+    __shared__ __attribute__((aligned(16))) uint32_t tab[4 * 256];
+    fill_plain(reinterpret_cast<uint8_t*>(tab), 0, &g_tab.pos[1 + kTinyRow0][0], 4 * 256);
+    __syncthreads();
+    const int lane = threadIdx.x;
+    const uint32_t* win32 = reinterpret_cast<const uint32_t*>(win);
+    constexpr uint32_t kUnits = kWalkWin / 16 + 1;   // 16-byte units per window (+ overhang)
+
+    for (uint64_t seg = blockIdx.x; seg < w.nseg; seg += gridDim.x) {
+        const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
+        const ramcrc_seg_cert cert = w.certs[seg];
+        uint32_t pos = 0, crc = 0xFFFFFFFFu, count = 0, flags = 0;
+        uint32_t wb = 0;
+        bool have = false;
+        u32x4 rec = {0u, 0u, 0u, 0u};
+        uint32_t nrec = 0;
+        auto flush = [&]() {
+            unsigned long long b = 0;
+            if (lane == 0)
+                b = atomicAdd(w.n_entries, (unsigned long long)nrec);
+            b = __shfl(b, 0, kWaveSize);
+            if (lane < int(nrec) && b + lane < w.cap)
+                w.entries[b + lane] = rec;
+            if (b + nrec > w.cap)
+                flags |= RAMCRC_SEG_TABLE_FULL;
+            nrec = 0;
+        };
+        uint64_t steps = 0;
+        while (pos < cert.segment_length && uint64_t(pos) < w.capacity) {
+            // deterministic walk below the capacity: more steps than bytes means
+            // a repeated position, i.e. the reference's loop never ends
+            if (++steps > w.capacity) {
+                flags |= RAMCRC_SEG_CYCLE;
+                break;
+            }
+            if (!have || pos - wb >= kWalkWin) {   // (a wrapped pos also reloads)
+                wb = pos & ~15u;
+                have = true;
+                __syncthreads();
+                for (uint32_t u = lane; u < kUnits; u += kWaveSize) {
+                    const uint64_t off = uint64_t(wb) + uint64_t(u) * 16;
+                    u32x4 v = {0u, 0u, 0u, 0u};
+                    if (off + 16 <= w.capacity)
+                        v = load16(sb + off);   // bytes past the capacity read as 0 (copyOut)
+                    *reinterpret_cast<u32x4*>(win + u * 16) = v;
+                }
+                __syncthreads();
+            }
+            const uint32_t o = pos - wb;
+            const uint32_t d0 = win32[o >> 2], d1 = win32[(o >> 2) + 1];
+            const uint64_t q = ((uint64_t(d1) << 32) | d0) >> (8 * (o & 3));
+            const uint32_t hdr = uint32_t(q) & 0xFF;
+            const uint32_t lb = (hdr >> 6) + 1;                       // getLengthBytes()
+            const uint32_t len = uint32_t(q >> 8) & (lb == 4 ? 0xFFFFFFFFu : ((1u << (8 * lb)) - 1));
+            if (lb == 4) {
+                crc = crc_small(tab, crc, uint32_t(q), 4);
+                crc = crc_small(tab, crc, uint32_t(q >> 32) & 0xFF, 1);
+            } else {   // 2-4 bytes: header + 1-3 length bytes
+                const uint32_t keep = lb == 3 ? 0xFFFFFFFFu : ((1u << (8 * (lb + 1))) - 1);
+                crc = crc_small(tab, crc, uint32_t(q) & keep, lb + 1);
+            }
+            const uint32_t next = pos + 1 + lb + len;   // uint32_t arithmetic, as the reference
+            if (uint64_t(next) > w.capacity) {
+                flags |= RAMCRC_SEG_PAST_CAPACITY;
+                break;
+            }
+            if (lane == int(nrec)) {
+                // a payload past the capacity is only reachable through the
+                // uint32_t wrap of the offset: flag it unreadable
+                const bool overlong = uint64_t(pos) + 1 + lb + len > w.capacity;
+                rec = u32x4{uint32_t(seg), pos, len, hdr | (overlong ? kRecOverlong : 0u)};
+            }
+            count++;
+            if (++nrec == uint32_t(kWaveSize))
+                flush();
+            pos = next;
+        }
+        if (nrec)
+            flush();
+        const uint32_t fin = ~crc_small(tab, crc, cert.segment_length, 4);
+        if (!(flags & (RAMCRC_SEG_PAST_CAPACITY | RAMCRC_SEG_CYCLE))) {
+            if (pos > cert.segment_length)
+                flags |= RAMCRC_SEG_PAST_LENGTH;
+            else if (fin == cert.checksum)
+                flags |= RAMCRC_SEG_OK;
+            else
+                flags |= RAMCRC_SEG_BAD_CHECKSUM;
+        }
+        if (lane == 0) {
+            ramcrc_seg_status st;
+            st.flags = flags;
+            st.checksum = fin;
+            st.entries = count;
+            st.bad_objects = 0;
+            w.status[seg] = st;
+        }
+    }
+}
+
+// ObjectManager::replaySegment's comparison (src/ObjectManager.cc:659-669):
+// computed object CRC vs. Object::Header::checksum (the payload's first 4 B).
+__global__ __launch_bounds__(256) void k_obj_compare(BatchDesc d, ramcrc_seg_status* status)
+{
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= entry_count<kRecords>(d))
+        return;
+    const u32x4 r = d.rec[i];
+    if ((r.w & 0x3f) != RAMCRC_LOG_ENTRY_TYPE_OBJ || !(d.seg_status[r.x].x & RAMCRC_SEG_OK))
+        return;
+    bool ok = false;
+    if (r.z >= kObjHeaderBytes && !(r.w & kRecOverlong)) {
+        const uint64_t payload = reinterpret_cast<uint64_t>(d.base) + uint64_t(r.x) * d.seg_bytes +
+                                 r.y + 1 + ((r.w >> 6) & 3) + 1;
+        const gu8* p = reinterpret_cast<const gu8*>(payload);
+        const uint32_t stored = uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) |
+                                (uint32_t(p[3]) << 24);
+        ok = d.out[i] == stored;
+    }
+    if (!ok)
+        atomicAdd(&status[r.x].bad_objects, 1u);
 }
 
 }  // namespace
@@ -2025,6 +2221,80 @@ int ramcrc_stream_host(ramcrc_ctx* c, const void* h_base, uint64_t seg_bytes, ui
         (void)hipEventDestroy(done[k]);
     }
     return rc;
+}
+
+
+int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride,
+                               uint32_t seg_capacity, uint64_t n_seg,
+                               const ramcrc_seg_cert* d_certs, ramcrc_seg_status* d_status,
+                               ramcrc_seg_entry* d_entries, uint64_t entries_cap,
+                               uint64_t* d_n_entries, void* stream)
+{
+    if (!c || !d_n_entries || (entries_cap && !d_entries))
+        return RAMCRC_EINVAL;
+    if (n_seg && (!d_base || !d_certs || !d_status))
+        return RAMCRC_EINVAL;
+    if ((reinterpret_cast<uintptr_t>(d_base) & 15) || (seg_stride & 15) || (seg_capacity & 15) ||
+        n_seg > 0xFFFFFFFFull || (n_seg > 1 && seg_stride < seg_capacity))
+        return RAMCRC_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    HIPCHK(hipMemsetAsync(d_n_entries, 0, sizeof(uint64_t), s));
+    if (n_seg == 0)
+        return RAMCRC_OK;
+    WalkDesc w{};
+    w.base = static_cast<const uint8_t*>(d_base);
+    w.stride = seg_stride;
+    w.capacity = seg_capacity;
+    w.nseg = n_seg;
+    w.certs = d_certs;
+    w.status = d_status;
+    w.entries = reinterpret_cast<u32x4*>(d_entries);
+    w.cap = entries_cap;
+    w.n_entries = reinterpret_cast<unsigned long long*>(d_n_entries);
+    uint64_t grid = n_seg;
+    if (grid > uint64_t(64) * c->ncu)
+        grid = uint64_t(64) * c->ncu;
+    hipLaunchKernelGGL(k_seg_walk, dim3(grid), dim3(kWaveSize), 0, s, w);
+    HIPCHK(hipGetLastError());
+    return RAMCRC_OK;
+}
+
+int ramcrc_verify_objects_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride,
+                                 const ramcrc_seg_entry* d_entries, uint64_t entries_cap,
+                                 const uint64_t* d_n_entries, uint32_t* d_obj_crc,
+                                 ramcrc_seg_status* d_status, void* stream)
+{
+    if (!c)
+        return RAMCRC_EINVAL;
+    if (entries_cap == 0)
+        return RAMCRC_OK;
+    if (!d_base || !d_entries || !d_n_entries || !d_obj_crc || !d_status)
+        return RAMCRC_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int rc = reserve_locked(c, default_chunk_bound(entries_cap), entries_cap);
+    if (rc)
+        return rc;
+    BatchDesc d{};
+    d.cshift = kChunkShift;
+    d.base = static_cast<const uint8_t*>(d_base);
+    d.seg_bytes = seg_stride;
+    d.n = entries_cap;
+    d.rec = reinterpret_cast<const u32x4*>(d_entries);
+    d.n_dev = d_n_entries;
+    d.seg_status = reinterpret_cast<const u32x4*>(d_status);
+    d.out = d_obj_crc;
+    d.flags = RAMCRC_FINALIZE;
+    rc = launch_planned<kRecords>(c, d, s);
+    if (rc)
+        return rc;
+    const uint64_t grid = (entries_cap + 255) / 256;
+    hipLaunchKernelGGL(k_obj_compare, dim3(grid), dim3(256), 0, s, d, d_status);
+    HIPCHK(hipGetLastError());
+    return RAMCRC_OK;
 }
 
 }  // extern "C"

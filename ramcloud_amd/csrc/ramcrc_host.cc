@@ -160,4 +160,56 @@ uint32_t ramcrc_combine(uint32_t raw_a, uint32_t raw_b, uint64_t len_b)
     return ramcrc_shift(raw_a, len_b) ^ raw_b;
 }
 
+// The append path of RecoverSegmentBenchmark::run
+// (nanobenchmarks/RecoverSegmentBenchmark.cc:131-146): Object(key, value,
+// version 0, timestamp 0) serialised by Object::assembleForLog
+// (src/Object.cc:213-218) -- Header{checksum, timestamp, version, tableId}
+// (src/Object.h:137-182), KeyCount 1, CumulativeKeyLength 8, the 8-byte key
+// (src/Object.cc:107-141), the value -- appended by Segment::append
+// (src/Segment.cc:197-228) while hasSpaceFor (:136-154) holds.
+int ramcrc_segment_fill_objects(uint8_t* seg, uint32_t capacity, uint32_t value_len,
+                                uint64_t first_key, uint32_t* n_objects, ramcrc_seg_cert* cert)
+{
+    if (!seg || !cert)
+        return RAMCRC_EINVAL;
+    const uint64_t objlen64 = 24 + 1 + 2 + 8 + uint64_t(value_len);
+    if (objlen64 > 0xFFFFFFFFull)
+        return RAMCRC_EINVAL;
+    const uint32_t objlen = uint32_t(objlen64);
+    const uint32_t lb = objlen < 0x100u ? 1 : objlen < 0x10000u ? 2 : objlen < 0x1000000u ? 3 : 4;
+    const uint8_t hdr = uint8_t(RAMCRC_LOG_ENTRY_TYPE_OBJ | ((lb - 1) << 6));
+    const uint64_t entry = 1 + lb + uint64_t(objlen);
+    uint32_t head = 0, n = 0, meta = 0xFFFFFFFFu;
+    uint64_t key = first_key;
+    while (entry <= uint64_t(capacity) - head) {
+        uint8_t* e = seg + head;
+        e[0] = hdr;
+        for (uint32_t k = 0; k < lb; k++)
+            e[1 + k] = uint8_t(objlen >> (8 * k));
+        meta = ramcrc_update(meta, e, 1 + lb);   // Segment's running metadata checksum
+        uint8_t* o = e + 1 + lb;
+        memset(o + 4, 0, 20);                    // timestamp, version, tableId
+        o[24] = 1;                               // KeyCount
+        o[25] = 8;                               // CumulativeKeyLength (LE)
+        o[26] = 0;
+        for (int k = 0; k < 8; k++)
+            o[27 + k] = uint8_t(key >> (8 * k));
+        const uint32_t ck = ~ramcrc_update(0xFFFFFFFFu, o + 4, objlen - 4);   // Object::computeChecksum
+        for (int k = 0; k < 4; k++)
+            o[k] = uint8_t(ck >> (8 * k));
+        head += uint32_t(entry);
+        n++;
+        key++;
+    }
+    memset(seg + head, 0, capacity - head);
+    uint8_t lenle[4];
+    for (int k = 0; k < 4; k++)
+        lenle[k] = uint8_t(head >> (8 * k));
+    cert->segment_length = head;
+    cert->checksum = ~ramcrc_update(meta, lenle, 4);   // Segment::getAppendedLength
+    if (n_objects)
+        *n_objects = n;
+    return RAMCRC_OK;
+}
+
 }  // extern "C"

@@ -57,6 +57,9 @@ def lib():
         "ramcrc_entries_device": (i32, [vp, vp, vp, vp, vp, vp, u64, u32, vp]),
         "ramcrc_batch_host": (i32, [vp, vp, vp, vp, vp, u64, u32]),
         "ramcrc_stream_host": (i32, [vp, vp, u64, u64, vp, u32, i32, i32]),
+        "ramcrc_segment_walk_device": (i32, [vp, vp, u64, u32, u64, vp, vp, vp, u64, vp, vp]),
+        "ramcrc_verify_objects_device": (i32, [vp, vp, u64, vp, u64, vp, vp, vp, vp]),
+        "ramcrc_segment_fill_objects": (i32, [vp, u32, u32, u64, _c.POINTER(u32), vp]),
         "ramcrc_ctx_set_timing": (i32, [vp, i32]),
         "ramcrc_ctx_scan_time": (i32, [vp, _c.POINTER(_c.c_double), _c.POINTER(u64)]),
         "ramcrc_ctx_status": (i32, [vp, _c.POINTER(u32)]),
@@ -127,6 +130,20 @@ def cpu_has_hw():
 
 def device_count():
     return int(lib().ramcrc_device_count())
+
+
+def segment_fill_objects(seg, value_len, first_key=0):
+    """Host append path: fill an empty segment (numpy uint8, pre-filled value
+    bytes) with RecoverSegmentBenchmark-shaped objects.  Returns
+    (n_objects, segment_length, checksum)."""
+    if not (isinstance(seg, np.ndarray) and seg.dtype == np.uint8 and seg.flags.c_contiguous):
+        raise RamcrcError("segment must be a contiguous numpy uint8 array")
+    n = _c.c_uint32(0)
+    cert = np.zeros(2, dtype=np.uint32)
+    rc = lib().ramcrc_segment_fill_objects(_c.c_void_p(seg.ctypes.data), seg.size, value_len,
+                                           first_key, _c.byref(n), _c.c_void_p(cert.ctypes.data))
+    _check(rc, "ramcrc_segment_fill_objects")
+    return n.value, int(cert[0]), int(cert[1])
 
 
 # ---------------------------------------------------------------- device
@@ -206,6 +223,26 @@ class Context:
                                          _ptr(out), n, FINALIZE if finalize else 0, _stream(stream))
         _check(rc, "ramcrc_entries_device")
         return out
+
+    def segment_walk(self, data, seg_stride, seg_capacity, nseg, certs, status, entries,
+                     n_entries, stream=None):
+        """Segment::checkMetadataIntegrity on the device.  certs: int32 [nseg, 2]
+        (segment_length, checksum); status: int32 [nseg, 4]; entries: int32
+        [cap, 4]; n_entries: int64 [1]."""
+        cap = 0 if entries is None else entries.shape[0]
+        rc = lib().ramcrc_segment_walk_device(self._h, _ptr(data), seg_stride, seg_capacity, nseg,
+                                              _ptr(certs), _ptr(status), _ptr(entries), cap,
+                                              _ptr(n_entries), _stream(stream))
+        _check(rc, "ramcrc_segment_walk_device")
+        return status
+
+    def verify_objects(self, data, seg_stride, entries, n_entries, obj_crc, status, stream=None):
+        """Object::computeChecksum + comparison for every object record of a walk."""
+        rc = lib().ramcrc_verify_objects_device(self._h, _ptr(data), seg_stride, _ptr(entries),
+                                                entries.shape[0], _ptr(n_entries), _ptr(obj_crc),
+                                                _ptr(status), _stream(stream))
+        _check(rc, "ramcrc_verify_objects_device")
+        return status
 
     def batch_host(self, buffers, init=None, finalize=True):
         """CRC a list of host buffers (bytes / numpy) on the GPU; returns np.uint32."""

@@ -1,0 +1,118 @@
+"""Recovery-segment verification on the GPU.
+
+What a backup's RecoverySegmentBuilder::build and a recovery master's
+ObjectManager::replaySegment do per replica, batched over many segments:
+
+  1. Segment::checkMetadataIntegrity (src/Segment.cc:758-800) -- walk the
+     length-prefixed entries, checksum their headers and lengths plus the
+     certificate length, compare with the SegmentCertificate;
+  2. for every object entry, Object::computeChecksum (src/Object.cc:805-819)
+     compared with the checksum stored in its header
+     (src/ObjectManager.cc:659-669).
+
+Both run in libramcrc's kernels (ramcrc_segment_walk_device,
+ramcrc_verify_objects_device); this module only allocates the tables and
+builds synthetic segments shaped like nanobenchmarks/RecoverSegmentBenchmark.cc
+(objects with 8-byte counter keys and splitmix64 value bytes) through the
+host append path ramcrc_segment_fill_objects.
+"""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+from . import ramcrc, workloads
+
+SEG_OK = 1
+SEG_PAST_CAPACITY = 2
+SEG_PAST_LENGTH = 4
+SEG_BAD_CHECKSUM = 8
+SEG_TABLE_FULL = 16
+SEG_CYCLE = 32
+LOG_ENTRY_TYPE_OBJ = 2
+
+REPLAY_SEED = 0x5245504C   # "REPL": value bytes of segment i use seed REPLAY_SEED + i
+OBJECT_OVERHEAD = 24 + 1 + 2 + 8   # Object::Header + KeyCount + CumulativeKeyLength + key
+
+
+def entry_bytes(value_len):
+    obj = OBJECT_OVERHEAD + value_len
+    lb = 1 if obj < 1 << 8 else 2 if obj < 1 << 16 else 3 if obj < 1 << 24 else 4
+    return 1 + lb + obj
+
+
+def objects_per_segment(capacity, value_len):
+    return capacity // entry_bytes(value_len)
+
+
+def fill_segments_host(buf, nseg, capacity, value_len, first_key=0, stride=None, threads=8):
+    """Turn nseg pre-filled segments of `buf` (numpy uint8; segment i at
+    i*stride) into object segments.  Keys continue across segments as in
+    RecoverSegmentBenchmark::run.  Returns certs uint32[nseg, 2] and the
+    object counts."""
+    stride = capacity if stride is None else stride
+    per = objects_per_segment(capacity, value_len)
+    certs = np.zeros((nseg, 2), np.uint32)
+    counts = np.zeros(nseg, np.uint32)
+
+    def one(i):
+        seg = buf[i * stride: i * stride + capacity]
+        n, length, ck = ramcrc.segment_fill_objects(seg, value_len, first_key + i * per)
+        certs[i] = (length, ck)
+        counts[i] = n
+
+    with ThreadPoolExecutor(max_workers=max(1, threads)) as ex:
+        list(ex.map(one, range(nseg)))
+    return certs, counts
+
+
+def object_segments_host(nseg, capacity, value_len, seed=REPLAY_SEED, threads=8):
+    """numpy buffer of nseg object segments (values = splitmix64 bytes of seed + i)."""
+    buf = np.empty(nseg * capacity, np.uint8)
+
+    def gen(i):
+        buf[i * capacity:(i + 1) * capacity] = workloads.splitmix_bytes_np(seed + i, capacity)
+
+    with ThreadPoolExecutor(max_workers=max(1, threads)) as ex:
+        list(ex.map(gen, range(nseg)))
+    certs, counts = fill_segments_host(buf, nseg, capacity, value_len, threads=threads)
+    return buf, certs, counts
+
+
+class RecoveryVerify:
+    """Device tables for walking and verifying batches of segments on one GPU.
+
+    verify(d_segments, certs) returns the per-segment status tensor
+    (int32 [nseg, 4]: flags, checksum, entries, bad_objects) after both
+    kernels ran on the current stream."""
+
+    def __init__(self, ctx, nseg, capacity, stride=None, entries_cap=None, min_entry=None):
+        import torch
+
+        self.ctx = ctx
+        self.nseg = nseg
+        self.capacity = capacity
+        self.stride = capacity if stride is None else stride
+        if entries_cap is None:
+            # every entry is at least a header byte, a length byte and an
+            # object header: enough for any segment of objects
+            min_entry = entry_bytes(0) if min_entry is None else min_entry
+            entries_cap = nseg * (capacity // min_entry + 1)
+        dev = torch.device("cuda", ctx.device)
+        self.entries = torch.zeros((entries_cap, 4), dtype=torch.int32, device=dev)
+        self.n_entries = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.obj_crc = torch.zeros(entries_cap, dtype=torch.int32, device=dev)
+        self.status = torch.zeros((nseg, 4), dtype=torch.int32, device=dev)
+
+    def walk(self, d_segments, d_certs, stream=None):
+        self.ctx.segment_walk(d_segments, self.stride, self.capacity, self.nseg, d_certs,
+                              self.status, self.entries, self.n_entries, stream=stream)
+        return self.status
+
+    def verify_objects(self, d_segments, stream=None):
+        self.ctx.verify_objects(d_segments, self.stride, self.entries, self.n_entries,
+                                self.obj_crc, self.status, stream=stream)
+        return self.status
+
+    def verify(self, d_segments, d_certs, stream=None):
+        self.walk(d_segments, d_certs, stream)
+        return self.verify_objects(d_segments, stream)
