@@ -169,20 +169,139 @@ def run_entries(args, ctx):
                 host=host, offs=offs, lens=lens, crcs=out.cpu().numpy().view(np.uint32))
 
 
+def run_replay(args, ctx):
+    """Recovery replay verify (RecoverSegmentBenchmark-shaped,
+    nanobenchmarks/RecoverSegmentBenchmark.cc:123-146): nseg 8 MiB segments
+    full of objects with 8-byte counter keys and value_len-byte values, built
+    by the host append path; one step = Segment::checkMetadataIntegrity of
+    every segment (src/Segment.cc:758-800) + Object::computeChecksum of every
+    object compared with its stored checksum (src/ObjectManager.cc:659-669)."""
+    from ramcloud_amd import segments
+    seg_bytes = args.seg_mib * MiB
+    nseg = args.replay_nseg
+    # value bytes: splitmix64 streams generated on the device, objects
+    # appended on the host (C append path, threads), copied back
+    d = torch.empty(nseg * seg_bytes, dtype=torch.uint8, device="cuda")
+    workloads.splitmix_fill_segments(d, seg_bytes, segments.REPLAY_SEED)
+    host = d.cpu().numpy()
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    certs, counts = segments.fill_segments_host(host, nseg, seg_bytes, args.value_len,
+                                                threads=threads)
+    d.copy_(torch.from_numpy(host))
+    dc = torch.from_numpy(np.ascontiguousarray(certs).view(np.int32)).cuda()
+    rv = segments.RecoveryVerify(ctx, nseg, seg_bytes, entries_cap=int(counts.sum()) + nseg)
+    for _ in range(args.warmup):
+        rv.verify(d, dc)
+    torch.cuda.synchronize()
+    ctx.set_timing(True)
+    ctx.scan_time()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st = rv.verify(d, dc)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    scan_ms, launches = ctx.scan_time()
+    ctx.set_timing(False)
+    status = st.cpu().numpy().view(np.uint32)
+    ok = bool((status[:, 0] == segments.SEG_OK).all() and (status[:, 3] == 0).all()
+              and np.array_equal(status[:, 2], counts)
+              and np.array_equal(status[:, 1], certs[:, 1]))
+    return dict(seg_bytes=seg_bytes, nseg=nseg, counts=counts, certs=certs, host=host,
+                elapsed=elapsed, scan_ms=scan_ms, launches=launches, ok=ok)
+
+
+def run_append(args, ctx):
+    """Batched write-path checksum (SURVEY.md 8(f) row 4): Object::assembleForLog
+    (src/Object.cc:213-238) over a batch of 1M serialized objects of the
+    config-3 sizes (100 B / 1 KiB / 4 KiB, Zipf), packed back to back in HBM;
+    one step = every header.checksum computed and stamped."""
+    from oracle import oracle
+    lens = workloads.entry_lengths(args.entries)
+    offs = workloads.packed_offsets(lens)
+    total = int(lens.sum())
+    host = workloads.splitmix_bytes_np(workloads.ENTRY_SEED, total)
+    data = torch.from_numpy(host).cuda()
+    off_t = torch.from_numpy(offs.view(np.int64)).cuda()
+    len_t = torch.from_numpy(lens.view(np.int64)).cuda()
+    out = torch.zeros(lens.size, dtype=torch.int32, device="cuda")
+    for _ in range(args.warmup):
+        ctx.assemble_objects(data, off_t, len_t, out)
+    torch.cuda.synchronize()
+    ctx.set_timing(True)
+    ctx.scan_time()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.assemble_objects(data, off_t, len_t, out)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    scan_ms, _ = ctx.scan_time()
+    ctx.set_timing(False)
+    credited = total - 4 * lens.size   # bytes [4, len) of every object
+    want = oracle.entries(host, offs + 4, lens - 4)
+    got = out.cpu().numpy().view(np.uint32)
+    stamped = data.cpu().numpy()
+    hdr = stamped[(offs.astype(np.int64)[:, None] + np.arange(4)).reshape(-1)].reshape(-1, 4).copy().view("<u4")[:, 0]
+    ok = bool(np.array_equal(got, want) and np.array_equal(hdr, want))
+    value = credited * args.steps / elapsed / 1e9
+    scan_s = scan_ms / args.steps / 1e3
+    achieved = credited / scan_s / 1e9 if scan_s > 0 else None
+    return {
+        "metric": "device-resident Object::assembleForLog checksum GB/s over 1M objects "
+                  "(100B/1KiB/4KiB Zipf)",
+        "value": round(value, 2), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic", "config": {"workload": f"{lens.size} objects, {total} bytes",
+                                        "credited_bytes": credited},
+        "roofline": {"bound": "hbm", "kernel": "k_entries",
+                     "achieved": round(achieved, 1) if achieved else None,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                     "traffic": None, "scan_ms_per_step": round(scan_s * 1e3, 4)},
+        "bit_exact_vs_oracle": ok,
+    }
+
+
+def replay_cpu_baseline(host, seg_bytes, certs, nsample):
+    """The restated reference walk + per-object verify (oracle, SSE4.2 CRC) on
+    nsample segments, one thread -- the checksum work of one
+    RecoverSegmentBenchmark replay thread."""
+    from oracle import oracle
+    t0 = time.perf_counter()
+    bad = 0
+    for i in range(nsample):
+        seg = host[i * seg_bytes:(i + 1) * seg_bytes]
+        f, ck, n, table = oracle.check_metadata(seg, int(certs[i, 0]), int(certs[i, 1]),
+                                                segment=0, table_cap=seg_bytes // 36 + 1)
+        b, _, _ = oracle.verify_objects(seg, seg_bytes, table, 1)
+        bad += b + (0 if f == 1 else 1)
+    dt = time.perf_counter() - t0
+    return {"value": round(nsample * seg_bytes / dt / 1e9, 3), "unit": "GB/s", "cores": 1,
+            "kind": "port",
+            "sample": f"{nsample} x {seg_bytes // MiB} MiB object segments, oracle restatement of "
+                      "Segment::checkMetadataIntegrity + Object::computeChecksum, 1 thread",
+            "all_verified": bad == 0}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="segments",
-                    choices=["segments", "recovery", "entries", "stream"])
+                    choices=["segments", "recovery", "entries", "stream", "replay", "append"])
     ap.add_argument("--nseg", type=int, default=1024, help="segments per GPU (weak scaling)")
     ap.add_argument("--nseg-total", type=int, default=2048, help="recovery config: total segments")
     ap.add_argument("--seg-mib", type=int, default=8)
     ap.add_argument("--entries", type=int, default=1_000_000)
     ap.add_argument("--path", default="entries", choices=["entries", "batch"])
     ap.add_argument("--entry-size", type=int, default=0, help="fixed entry length (default: Zipf mix)")
+    ap.add_argument("--replay-nseg", type=int, default=512,
+                    help="replay config: segments (RecoverSegmentBenchmark: 4096/8)")
+    ap.add_argument("--value-len", type=int, default=1024, help="replay config: object value bytes")
     ap.add_argument("--cpu-sample", type=int, default=128, help="segments timed on the CPU")
+    ap.add_argument("--replay-cpu-sample", type=int, default=16,
+                    help="replay config: segments verified by the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -278,6 +397,36 @@ def main():
                          "scan_ms_per_step": round(scan_s_per_step * 1e3, 4)},
             "bit_exact_vs_oracle": ok,
         }
+    elif args.config == "replay":
+        from ramcloud_amd import segments
+        r = run_replay(args, ctx)
+        seg_total = r["nseg"] * r["seg_bytes"]
+        value = seg_total * args.steps / r["elapsed"] / 1e9
+        obj_bytes = int(r["counts"].sum()) * (segments.OBJECT_OVERHEAD + args.value_len - 4)
+        scan_s_per_step = r["scan_ms"] / args.steps / 1e3
+        achieved = obj_bytes / scan_s_per_step / 1e9 if scan_s_per_step > 0 else None
+        cpu = None if args.no_cpu_baseline else replay_cpu_baseline(
+            r["host"], r["seg_bytes"], r["certs"], min(args.replay_cpu_sample, r["nseg"]))
+        line = {
+            "metric": "device-resident recovery replay verify GB/s of 8 MiB object segments "
+                      "(segment walk + per-object checksum compare)",
+            "value": round(value, 2), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (RecoverSegmentBenchmark-shaped objects, splitmix64 values)",
+            "config": {"workload": f"{r['nseg']} x {args.seg_mib} MiB segments of "
+                                   f"{args.value_len} B-value objects",
+                       "objects": int(r["counts"].sum()), "object_bytes_checksummed": obj_bytes},
+            "roofline": {"bound": "hbm", "kernel": "k_entries (object verify)",
+                         "achieved": round(achieved, 1) if achieved else None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                         "traffic": None, "scan_ms_per_step": round(scan_s_per_step * 1e3, 4)},
+            "cpu_baseline": cpu,
+            "all_segments_verified": r["ok"],
+        }
+    elif args.config == "append":
+        line = run_append(args, ctx)
     else:  # stream (config 5): host-to-host
         seg_bytes = args.seg_mib * MiB
         nseg = args.nseg

@@ -104,6 +104,27 @@ class Crc32CBatch {
               "ramcrc_batch_device");
     }
 
+    /**
+     * Object::assembleForLog's checksum for a batch of serialized objects
+     * (the write path, src/ObjectManager.cc:1274): header.checksum of every
+     * object (Object::Header + keysAndValue, src/Object.h:137-182) is set to
+     * Object::computeChecksum() (src/Object.cc:770-819), computed on the GPU.
+     * Objects shorter than the header are left unchanged.  Synchronous.
+     */
+    void
+    assembleObjects(const std::vector<std::pair<void*, uint64_t> >& objects)
+    {
+        std::vector<void*> ptrs;
+        std::vector<uint64_t> lens;
+        for (size_t i = 0; i < objects.size(); i++) {
+            ptrs.push_back(objects[i].first);
+            lens.push_back(objects[i].second);
+        }
+        if (!objects.empty())
+            check(ramcrc_assemble_objects_host(context(), &ptrs[0], &lens[0], ptrs.size()),
+                  "ramcrc_assemble_objects_host");
+    }
+
   private:
     ramcrc_ctx*
     context()

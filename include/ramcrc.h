@@ -204,6 +204,28 @@ int ramcrc_verify_objects_device(ramcrc_ctx* ctx, const void* d_base, uint64_t s
 int ramcrc_segment_fill_objects(uint8_t* seg, uint32_t capacity, uint32_t value_len,
                                 uint64_t first_key, uint32_t* n_objects, ramcrc_seg_cert* cert);
 
+/* ------------------------------------------------- batched write path --- */
+
+/* Object::assembleForLog's checksum (src/Object.cc:213-238; the value is
+ * Object::computeChecksum, src/Object.cc:770-819) for a batch of serialized
+ * objects in device memory, e.g. the objects of a multi-write batch before
+ * Log::append (src/ObjectManager.cc:1274-1297): object i is d_len[i] bytes at
+ * d_base + d_off[i] -- Object::Header {checksum, timestamp, version, tableId}
+ * (src/Object.h:137-182) followed by keysAndValue.  For every object of at
+ * least the 24-byte header, the finalized CRC32C of bytes [4, len) is stored
+ * little-endian into bytes [0, 4) (Header::checksum) and into d_out[i] when
+ * d_out is not NULL; shorter objects are left unchanged (d_out[i] = 0).
+ * Objects must not overlap.  Stream-ordered. */
+int ramcrc_assemble_objects_device(ramcrc_ctx* ctx, void* d_base, const uint64_t* d_off,
+                                   const uint64_t* d_len, uint32_t* d_out, uint64_t n,
+                                   void* stream);
+
+/* The same for objects in host memory (a write batch still in its RPC
+ * buffers): staged through pinned memory, CRCs computed on the GPU, each
+ * Header::checksum written back into the host object.  Synchronous. */
+int ramcrc_assemble_objects_host(ramcrc_ctx* ctx, void* const* objs, const uint64_t* lens,
+                                 uint64_t n);
+
 /* Kernel timing (for benchmarks): when enabled, every launch brackets its
  * byte-scan kernel (k_chunks, or k_entries on the small path) with HIP events
  * on the launch stream.  ramcrc_ctx_scan_time waits for the recorded events,

@@ -426,7 +426,10 @@ uint64_t oracle_verify_objects(const uint8_t* base, uint64_t stride, const uint3
         int ok = 0;
         if (r[2] >= 24 && !(r[3] & 0x100)) {
             const uint8_t* payload = base + (uint64_t)r[0] * stride + r[1] + 1 + ((r[3] >> 6) & 3) + 1;
-            uint32_t c = ~oracle_slicing8(0xFFFFFFFFu, payload + 4, r[2] - 4);
+            /* Crc32C picks the crc32 instruction when the CPU has it
+             * (src/Crc32C.h:200-206); both forms agree bit for bit */
+            const crc_fn f = oracle_have_sse42() ? oracle_sse42 : oracle_slicing8;
+            uint32_t c = ~f(0xFFFFFFFFu, payload + 4, r[2] - 4);
             if (crc_out)
                 crc_out[i] = c;
             ok = c == oracle_u32le(payload);

@@ -73,6 +73,7 @@ constexpr uint32_t kBlock = 1024;                  // bytes per wave step
 constexpr int kChunkShift = RAMCRC_CHUNK_SHIFT;
 constexpr uint64_t kChunk = 1ull << kChunkShift;   // 256 KiB per wave work item
 constexpr uint64_t kLargeMin = 64 * 1024;          // batch API threshold
+constexpr uint64_t kWideCombineMin = 16384;        // tables above: k_combine<kWide>
 constexpr int kUnroll = RAMCRC_UNROLL;             // blocks per register group (x2 in flight)
 constexpr bool kDynamic = RAMCRC_DYNAMIC;          // waves dequeue chunks from a counter
 
@@ -85,6 +86,7 @@ struct alignas(16) DeviceTables {
     uint32_t xblk[4][256];  // x^(8 * 1024 * b * 256^j)
     uint32_t xinv[1024];    // x^(-8 p)
     uint32_t pos[132][256]; // k_entries_tiny: row r = X^(r-3)(byte), rows 0..3 (m <= 0) zero
+    uint32_t xmeta[5 * 64 + 1];   // k_seg_walk: x^(8d), d = 0 .. 320 (one batch of metadata)
 };
 
 constexpr DeviceTables make_device_tables()
@@ -115,6 +117,8 @@ constexpr DeviceTables make_device_tables()
         for (uint32_t b = 0; b < 256; b++)
             t.pos[m + 3][b] = ramcrc::mulmod(b, c);
     }
+    for (int d = 0; d <= 5 * 64; d++)
+        t.xmeta[d] = ramcrc::xpow8(uint64_t(d));
     return t;
 }
 
@@ -305,6 +309,16 @@ __device__ __forceinline__ uint32_t fix_word(uint32_t w, uint64_t a, uint64_t S,
     return w ^ ((dd > -4 && dd < 4) ? inj : 0u);
 }
 
+// Wave-uniform 64-bit value into scalar registers.  (The builtin returns a
+// signed int: each half goes through uint32_t, or the low half would
+// sign-extend into the high one.)
+__device__ __forceinline__ uint64_t rfl64(uint64_t v)
+{
+    const uint32_t lo = uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(v)));
+    const uint32_t hi = uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(v >> 32)));
+    return (uint64_t(hi) << 32) | lo;
+}
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // Explicit global address space: generic (flat_*) loads would also count in
 // lgkmcnt and serialise against the LDS table lookups.
@@ -346,7 +360,11 @@ struct BatchDesc {
 //                the segment (kRecOverlong), and every record of a segment
 //                whose metadata check failed (RecoverySegmentBuilder::build
 //                stops there, src/RecoverySegmentBuilder.cc:61-203).
-enum Mode { kSegAligned = 0, kSegUniform = 1, kTable = 2, kRecords = 3 };
+//   kObjects:    buffer i = bytes [4, len[i]) of the serialized object at
+//                base + off[i] (Object::computeChecksum on the write path,
+//                Object::assembleForLog, src/Object.cc:213-238); objects
+//                shorter than their 24-byte header are inactive.
+enum Mode { kSegAligned = 0, kSegUniform = 1, kTable = 2, kRecords = 3, kObjects = 4 };
 
 constexpr uint32_t kObjHeaderBytes = 24;   // Object::Header, src/Object.h:137-182
 constexpr uint32_t kRecOverlong = 0x100;   // record header bit: payload past the capacity
@@ -375,6 +393,12 @@ __device__ __forceinline__ bool buffer_range(const BatchDesc& d, uint64_t i, uin
         S = payload + 4;
         E = obj ? payload + r.z : S;
         return obj;
+    } else if (kMode == kObjects) {
+        const uint64_t o = reinterpret_cast<uint64_t>(d.base) + d.off[i];
+        const uint64_t L = d.len[i];
+        S = o + 4;
+        E = L >= kObjHeaderBytes ? o + L : S;
+        return L >= kObjHeaderBytes;
     } else if (kMode != kTable) {
         S = reinterpret_cast<uint64_t>(d.base) + i * d.seg_bytes;
         E = S + d.seg_bytes;
@@ -566,8 +590,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_chunks(BatchDesc d, Plan pl, ui
         uint64_t t = 0;
         if (lane == 0)
             t = atomicAdd(pl.ticket, 1ull);
-        return __builtin_amdgcn_readfirstlane(uint32_t(t)) |
-               (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(t >> 32))) << 32);
+        return rfl64(t);
     };
     uint64_t g = kDynamic ? take() : wave;
     while (g < total) {
@@ -594,22 +617,21 @@ __global__ __launch_bounds__(kThreads, 1) void k_chunks(BatchDesc d, Plan pl, ui
     }
 }
 
-// ------------------------------------------------------------ k_combine
-template <int kMode>
-__global__ __launch_bounds__(256) void k_combine(BatchDesc d, Plan pl, uint64_t per_seg)
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src)
 {
-    const int lane = threadIdx.x & (kWaveSize - 1);
-    const uint64_t i = uint64_t(blockIdx.x) * (256 / kWaveSize) + threadIdx.x / kWaveSize;
-    if (blockIdx.x == 0 && threadIdx.x == 0)
-        *pl.ticket = 0;   // k_chunks of this launch is complete (same stream)
-    if (i >= entry_count<kMode>(d))
-        return;
-    uint64_t S, E;
-    buffer_range<kMode>(d, i, S, E);
-    if (!is_large(E - S))
-        return;   // handled by k_entries (or inactive)
-    if (kMode != kSegAligned && ((*pl.status) & 1u))
-        return;   // k_chunks refused the launch (partials overflow)
+    const uint32_t lo = __shfl(uint32_t(v), src, kWaveSize);
+    const uint32_t hi = __shfl(uint32_t(v >> 32), src, kWaveSize);
+    return (uint64_t(hi) << 32) | lo;
+}
+
+// ------------------------------------------------------------ k_combine
+// Merge the chunk partials of large buffer i (one wave): lane k multiplies
+// partial k by x^(8 * 1024 * t), t = its distance to the padded end in 1 KiB
+// units; XOR across lanes; x^(-8 pad) removes the padding of the last block.
+template <int kMode>
+__device__ __forceinline__ void combine_one(const BatchDesc& d, const Plan& pl, uint64_t per_seg,
+                                            uint64_t i, uint64_t S, uint64_t E, int lane)
+{
     const uint64_t g0 = kMode == kSegAligned ? i * per_seg
                                              : pl.group_pref[i / kThreads] + pl.local[i];
     const uint64_t cnt = chunk_count(S, E, d.cshift);
@@ -630,6 +652,42 @@ __global__ __launch_bounds__(256) void k_combine(BatchDesc d, Plan pl, uint64_t 
         R = mulmod_dev(R, g_tab.xinv[pad]);
     if (lane == 0)
         d.out[i] = (d.flags & RAMCRC_FINALIZE) ? ~R : R;
+}
+
+// kWide = false: one wave per buffer (few buffers, most of them large).
+// kWide = true:  one wave per 64 buffers -- each lane tests one, the wave
+// merges the large ones it found -- for big tables of mostly small entries,
+// where a wave per entry would cost more than the entries' own scan.
+template <int kMode, bool kWide>
+__global__ __launch_bounds__(256) void k_combine(BatchDesc d, Plan pl, uint64_t per_seg)
+{
+    const int lane = threadIdx.x & (kWaveSize - 1);
+    const uint64_t wave = uint64_t(blockIdx.x) * (256 / kWaveSize) + threadIdx.x / kWaveSize;
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        *pl.ticket = 0;   // k_chunks of this launch is complete (same stream)
+    if (kMode != kSegAligned && ((*pl.status) & 1u))
+        return;   // k_chunks refused the launch (partials overflow)
+    const uint64_t n = entry_count<kMode>(d);
+    if (!kWide) {
+        if (wave >= n)
+            return;
+        uint64_t S, E;
+        buffer_range<kMode>(d, wave, S, E);
+        if (is_large(E - S))   // (small ones: k_entries; inactive ones: none)
+            combine_one<kMode>(d, pl, per_seg, wave, S, E, lane);
+        return;
+    }
+    if (pl.group_pref[pl.ngroups] == 0)
+        return;   // no large buffer in this launch
+    const uint64_t i = wave * kWaveSize + lane;
+    uint64_t S = 0, E = 0;
+    const bool big = i < n && buffer_range<kMode>(d, i, S, E) && is_large(E - S);
+    uint64_t todo = __ballot(big);
+    while (todo) {
+        const int j = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        combine_one<kMode>(d, pl, per_seg, wave * kWaveSize + j, shfl64(S, j), shfl64(E, j), lane);
+    }
 }
 
 // ------------------------------------------------------------ k_entries
@@ -897,12 +955,6 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter(BatchDesc d, Sorted so
     }
 }
 
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src)
-{
-    const uint32_t lo = __shfl(uint32_t(v), src, kWaveSize);
-    const uint32_t hi = __shfl(uint32_t(v >> 32), src, kWaveSize);
-    return (uint64_t(hi) << 32) | lo;
-}
 
 // Mask and init-inject the 16 bytes of lane piece `a` of entry [S, E): one
 // 64-bit clamp per piece, then 32-bit arithmetic per word.
@@ -1026,7 +1078,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_entries_tiny(BatchDesc d, Sorte
             const uint64_t E = (uint64_t(dd.w) << 32) | dd.z;
             const uint64_t A = S & ~uint64_t(15);
             const uint64_t a = A + gl * 16;
-            // geo: len (bits 0-7, < 256), S - a + 128 (8-15), E - a + 128 (16-23)
+            // geo: len (bits 0-7, <= 128), S - a + 128 (8-15), E - a + 128 (16-24: up
+            // to 256, when the entry ends exactly at the end of its window)
             geo[q] = uint32_t(E - S) | (uint32_t(int(int64_t(S - a)) + 128) << 8) |
                      (uint32_t(int(int64_t(E - a)) + 128) << 16);
             const bool big = E - S >= 4;
@@ -1037,7 +1090,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_entries_tiny(BatchDesc d, Sorte
         for (int q = 0; q < 8; q++) {
             const uint32_t len = geo[q] & 0xFF;
             const int ds = int((geo[q] >> 8) & 0xFF) - 128;    // S - a (<= 15)
-            const int e = int((geo[q] >> 16) & 0xFF) - 128;    // E - a (<= 128)
+            const int e = int((geo[q] >> 16) & 0x1FF) - 128;   // E - a (<= 128)
             uint32_t R = 0;
             if (len >= 4) {
                 // Byte at distance m from E contributes row m + 3; bytes at or
@@ -1500,6 +1553,9 @@ struct ramcrc_ctx {
     uint32_t* sidx = nullptr;
     uint32_t* sinit = nullptr;
     uint64_t sorted_cap = 0;
+    // per-object checksums of ramcrc_assemble_objects_device when d_out is NULL
+    uint32_t* obj_out = nullptr;
+    uint64_t obj_out_cap = 0;
     // host staging for ramcrc_batch_host / ramcrc_stream_host
     uint8_t* h_stage = nullptr;
     uint64_t h_stage_cap = 0;
@@ -1669,7 +1725,12 @@ int launch_planned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s)
                            uint64_t(0));
     }
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_combine<kMode>, dim3((d.n + 3) / 4), dim3(256), 0, s, d, pl, uint64_t(0));
+    if (d.n > kWideCombineMin)
+        hipLaunchKernelGGL((k_combine<kMode, true>), dim3((d.n + 255) / 256), dim3(256), 0, s, d, pl,
+                           uint64_t(0));
+    else
+        hipLaunchKernelGGL((k_combine<kMode, false>), dim3((d.n + 3) / 4), dim3(256), 0, s, d, pl,
+                           uint64_t(0));
     HIPCHK(hipGetLastError());
     return launch_binned<kMode>(c, d, s, 1);
 }
@@ -1677,16 +1738,26 @@ int launch_planned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s)
 // ------------------------------------------------------------ segment walk
 // Segment::checkMetadataIntegrity (src/Segment.cc:758-800) on the device: one
 // wavefront per segment.  The walk is a pointer chase through length-prefixed
-// entries (|EntryHeader|length 1-4 B|payload|, src/Segment.h:99-112), so it is
-// latency-bound, not bandwidth-bound: the wave stages a 16 KiB window of the
-// segment in LDS around the current entry header (coalesced loads), and the
-// chase runs on LDS reads; an entry larger than the window makes the next
-// window start at the next header, so payload bytes are never fetched.  The
-// metadata checksum (header byte + length bytes of every entry, then the
-// certificate length) is updated with <= 4-byte slicing steps from LDS tables.
+// entries (|EntryHeader|length 1-4 B|payload|, src/Segment.h:99-112): latency,
+// not bandwidth, bounds it, so everything is arranged to keep one hop short.
+//  * The chase reads only LDS.  The segment is staged through 16 KiB windows
+//    (coalesced 1 KiB wave loads); while one window is walked the next one is
+//    already in flight in registers.  Consecutive windows overlap by 16 bytes,
+//    so an entry header and its length bytes (<= 5 B, read as 8) never
+//    straddle two windows.  An entry that jumps past the prefetched window
+//    reloads at its header: payload bytes of large entries are never fetched.
+//  * The metadata checksum is off the chase.  A hop only parks its entry in
+//    one lane; every 64 hops the wave checksums the 64 parked header+length
+//    byte strings in parallel -- lane j: raw(0, bytes_j) moved past the bytes
+//    of the entries after it (x^(8d) from a table, one GF(2) multiply) --
+//    XORs them across the wave and folds the batch into the running state:
+//    raw(s, A||B) = X^|B|(raw(s, A)) ^ raw(0, B).
 // Complete entries are appended to the record table 64 at a time (one atomic
 // per 64 records).
-constexpr uint32_t kWalkWin = 16384;
+constexpr uint32_t kWalkWin = 16384;                          // bytes per window
+constexpr uint32_t kWalkStep = kWalkWin - 16;                 // window advance
+constexpr int kWalkPer = int(kWalkWin / 16 / kWaveSize);      // 16-byte units per lane
+constexpr uint32_t kWalkMeta = 5 * kWaveSize;                 // metadata bytes per batch, max
 
 struct WalkDesc {
     const uint8_t* base;
@@ -1712,87 +1783,180 @@ __device__ __forceinline__ uint32_t crc_small(const uint32_t* t, uint32_t c, uin
     return r;
 }
 
+// Issue the loads of window [wbase, wbase + kWalkWin) of a segment (lane l:
+// units l + 64 k) as buffer loads whose descriptor ends at the segment's
+// capacity: units past it read as zero with no branch, as Segment::copyOut
+// leaves bytes past the segment's end.
+__device__ __forceinline__ void walk_issue(u32x4 (&r)[kWalkPer], uint64_t sb, uint64_t wbase,
+                                           uint64_t capacity, int lane)
+{
+    const uint64_t base = rfl64(sb + wbase);
+    const uint32_t nrec =
+        __builtin_amdgcn_readfirstlane(uint32_t(wbase < capacity ? capacity - wbase : 0));
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), (short)0, int(nrec),
+                                          0x00020000);
+#pragma unroll
+    for (int k = 0; k < kWalkPer; k++)
+        r[k] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, uint32_t(lane + kWaveSize * k) * 16, 0, 0);
+}
+
+__device__ __forceinline__ void walk_store(uint8_t* win, const u32x4 (&r)[kWalkPer], int lane)
+{
+#pragma unroll
+    for (int k = 0; k < kWalkPer; k++)
+        *reinterpret_cast<u32x4*>(win + (lane + kWaveSize * k) * 16) = r[k];
+}
+
 __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t win[kWalkWin + 16];
+    __shared__ __attribute__((aligned(16))) uint8_t win[2][kWalkWin];
     __shared__ __attribute__((aligned(16))) uint32_t tab[4 * 256];
+    __shared__ uint32_t xm[kWalkMeta + 1];
     fill_plain(reinterpret_cast<uint8_t*>(tab), 0, &g_tab.pos[1 + kTinyRow0][0], 4 * 256);
+    for (uint32_t t = threadIdx.x; t <= kWalkMeta; t += blockDim.x)
+        xm[t] = g_tab.xmeta[t];
     __syncthreads();
     const int lane = threadIdx.x;
-    const uint32_t* win32 = reinterpret_cast<const uint32_t*>(win);
-    constexpr uint32_t kUnits = kWalkWin / 16 + 1;   // 16-byte units per window (+ overhang)
 
     for (uint64_t seg = blockIdx.x; seg < w.nseg; seg += gridDim.x) {
         const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
         const ramcrc_seg_cert cert = w.certs[seg];
         uint32_t pos = 0, crc = 0xFFFFFFFFu, count = 0, flags = 0;
-        uint32_t wb = 0;
-        bool have = false;
-        u32x4 rec = {0u, 0u, 0u, 0u};
-        uint32_t nrec = 0;
-        auto flush = [&]() {
-            unsigned long long b = 0;
-            if (lane == 0)
-                b = atomicAdd(w.n_entries, (unsigned long long)nrec);
-            b = __shfl(b, 0, kWaveSize);
-            if (lane < int(nrec) && b + lane < w.cap)
-                w.entries[b + lane] = rec;
-            if (b + nrec > w.cap)
-                flags |= RAMCRC_SEG_TABLE_FULL;
-            nrec = 0;
+        // Parked entries: lane j holds entry j of the current batch of 64.
+        uint32_t rpos = 0, rlen = 0, rinfo = 0;
+        uint32_t ns = 0;
+
+        // Fold the parked entries' header + length bytes into crc and append
+        // the first nrec of them to the record table.
+        auto flush = [&](uint32_t nrec) {
+            uint32_t m = 0, r = 0;
+            if (lane < int(ns)) {
+                const uint32_t hdr = rinfo & 0xFF, lb = (hdr >> 6) + 1;
+                m = 1 + lb;
+                r = crc_small(tab, 0u, hdr | (rlen << 8), m < 4 ? m : 4);
+                if (m == 5)
+                    r = crc_small(tab, r, rlen >> 24, 1);
+            }
+            uint32_t incl = m;   // inclusive prefix of the byte counts
+#pragma unroll
+            for (int s = 1; s < kWaveSize; s <<= 1) {
+                const uint32_t y = __shfl_up(incl, s, kWaveSize);
+                if (lane >= s)
+                    incl += y;
+            }
+            const uint32_t total = __shfl(incl, kWaveSize - 1, kWaveSize);
+            uint32_t c = lane < int(ns) ? mulmod_horner(r, xm[total - incl]) : 0u;
+#pragma unroll
+            for (int s = 1; s < kWaveSize; s <<= 1)
+                c ^= __shfl_xor(c, s, kWaveSize);
+            crc = mulmod_horner(crc, xm[total]) ^ c;
+            if (nrec) {
+                unsigned long long b = 0;
+                if (lane == 0)
+                    b = atomicAdd(w.n_entries, (unsigned long long)nrec);
+                b = __shfl(b, 0, kWaveSize);
+                if (lane < int(nrec) && b + lane < w.cap)
+                    w.entries[b + lane] = u32x4{uint32_t(seg), rpos, rlen, rinfo};
+                if (b + nrec > w.cap)
+                    flags |= RAMCRC_SEG_TABLE_FULL;
+            }
+            ns = 0;
         };
-        uint64_t steps = 0;
-        while (pos < cert.segment_length && uint64_t(pos) < w.capacity) {
+
+        // window state: win[cur] holds [wb, wb + kWalkWin); pf is loading
+        // [wb + kWalkStep, ...)
+        int cur = 0;
+        uint32_t wb = 0;
+        u32x4 pf[kWalkPer];
+        __syncthreads();   // the previous segment's LDS reads are done
+        walk_issue(pf, sb, 0, w.capacity, lane);
+        walk_store(win[0], pf, lane);
+        walk_issue(pf, sb, kWalkStep, w.capacity, lane);
+        __syncthreads();
+
+        // The chase: every value below is wave-uniform (scalar registers).
+        // The outer loop moves windows, flushes full batches and stops the
+        // walk; the inner loop is the hop itself -- one LDS read and a few
+        // scalar operations -- and runs while the entry header stays inside
+        // the window, the batch has room and the cycle bound is not reached.
+        const uint32_t cap32 = uint32_t(w.capacity);
+        const uint32_t limit = cert.segment_length < cap32 ? cert.segment_length : cap32;
+        uint32_t steps = 0;
+        bool overrun = false;
+        while (pos < limit) {
             // deterministic walk below the capacity: more steps than bytes means
             // a repeated position, i.e. the reference's loop never ends
-            if (++steps > w.capacity) {
+            if (steps >= cap32) {
                 flags |= RAMCRC_SEG_CYCLE;
                 break;
             }
-            if (!have || pos - wb >= kWalkWin) {   // (a wrapped pos also reloads)
-                wb = pos & ~15u;
-                have = true;
-                __syncthreads();
-                for (uint32_t u = lane; u < kUnits; u += kWaveSize) {
-                    const uint64_t off = uint64_t(wb) + uint64_t(u) * 16;
-                    u32x4 v = {0u, 0u, 0u, 0u};
-                    if (off + 16 <= w.capacity)
-                        v = load16(sb + off);   // bytes past the capacity read as 0 (copyOut)
-                    *reinterpret_cast<u32x4*>(win + u * 16) = v;
+            if (pos - wb > kWalkWin - 8) {   // (a position below wb wraps: reload)
+                const uint64_t nb = uint64_t(wb) + kWalkStep;
+                if (uint64_t(pos) >= nb && uint64_t(pos) - nb <= kWalkWin - 8) {
+                    walk_store(win[cur ^ 1], pf, lane);   // the prefetched window
+                    cur ^= 1;
+                    wb = uint32_t(nb);
+                } else {                                    // a jump: reload at the header
+                    wb = pos & ~15u;
+                    walk_issue(pf, sb, wb, w.capacity, lane);
+                    walk_store(win[cur], pf, lane);
                 }
                 __syncthreads();
+                walk_issue(pf, sb, uint64_t(wb) + kWalkStep, w.capacity, lane);
             }
-            const uint32_t o = pos - wb;
-            const uint32_t d0 = win32[o >> 2], d1 = win32[(o >> 2) + 1];
-            const uint64_t q = ((uint64_t(d1) << 32) | d0) >> (8 * (o & 3));
-            const uint32_t hdr = uint32_t(q) & 0xFF;
-            const uint32_t lb = (hdr >> 6) + 1;                       // getLengthBytes()
-            const uint32_t len = uint32_t(q >> 8) & (lb == 4 ? 0xFFFFFFFFu : ((1u << (8 * lb)) - 1));
-            if (lb == 4) {
-                crc = crc_small(tab, crc, uint32_t(q), 4);
-                crc = crc_small(tab, crc, uint32_t(q >> 32) & 0xFF, 1);
-            } else {   // 2-4 bytes: header + 1-3 length bytes
-                const uint32_t keep = lb == 3 ? 0xFFFFFFFFu : ((1u << (8 * (lb + 1))) - 1);
-                crc = crc_small(tab, crc, uint32_t(q) & keep, lb + 1);
+            if (ns == uint32_t(kWaveSize))
+                flush(ns);
+            const uint32_t* w32 = reinterpret_cast<const uint32_t*>(win[cur]);
+            // hop while pos - wb <= span (header + 7 bytes inside the window, pos
+            // below the limit) and the batch and the cycle bound have room
+            const uint64_t wend = uint64_t(wb) + (kWalkWin - 8);
+            const uint32_t last = limit - 1 < wend ? limit - 1 : uint32_t(wend);
+            const uint32_t span = last - wb;
+            uint32_t room = uint32_t(kWaveSize) - ns;
+            if (cap32 - steps < room)
+                room = cap32 - steps;
+            for (uint32_t k = 0; k < room; k++) {
+                const uint32_t o = pos - wb;
+                const uint32_t d0 = __builtin_amdgcn_readfirstlane(w32[o >> 2]);
+                const uint32_t d1 = __builtin_amdgcn_readfirstlane(w32[(o >> 2) + 1]);
+                const uint64_t q = ((uint64_t(d1) << 32) | d0) >> (8 * (o & 3));
+                const uint32_t hdr = uint32_t(q) & 0xFF;
+                const uint32_t lb = (hdr >> 6) + 1;                       // getLengthBytes()
+                const uint32_t len = uint32_t(q >> 8) & (0xFFFFFFFFu >> (32 - 8 * lb));
+                // next = pos + 1 + lb + len in uint32_t arithmetic, as the
+                // reference; pos + 1 + lb cannot wrap (pos < capacity < 2^32 - 16).
+                // A payload past the capacity is only reachable through the
+                // wrap (carry out of 32 bits): flagged unreadable.
+                const uint32_t hl = pos + 1 + lb;
+                uint32_t next, ovl;
+                // scalar add with carry (the compiler would route the carry
+                // through a VALU add and back)
+                asm("s_add_u32 %0, %2, %3\n\ts_cselect_b32 %1, 0x100, 0"
+                    : "=s"(next), "=s"(ovl) : "s"(hl), "s"(len) : "scc");
+                const uint32_t info = hdr | ovl;   // kRecOverlong
+                const bool mine = lane == int(ns);   // park: one compare, three selects
+                rpos = mine ? pos : rpos;
+                rlen = mine ? len : rlen;
+                rinfo = mine ? info : rinfo;
+                ns++;
+                steps++;
+                if (next > cap32) {
+                    // its header and length were checksummed; it is not a record
+                    flags |= RAMCRC_SEG_PAST_CAPACITY;
+                    overrun = true;
+                    break;
+                }
+                pos = next;
+                if (pos - wb > span)
+                    break;
             }
-            const uint32_t next = pos + 1 + lb + len;   // uint32_t arithmetic, as the reference
-            if (uint64_t(next) > w.capacity) {
-                flags |= RAMCRC_SEG_PAST_CAPACITY;
+            if (overrun)
                 break;
-            }
-            if (lane == int(nrec)) {
-                // a payload past the capacity is only reachable through the
-                // uint32_t wrap of the offset: flag it unreadable
-                const bool overlong = uint64_t(pos) + 1 + lb + len > w.capacity;
-                rec = u32x4{uint32_t(seg), pos, len, hdr | (overlong ? kRecOverlong : 0u)};
-            }
-            count++;
-            if (++nrec == uint32_t(kWaveSize))
-                flush();
-            pos = next;
         }
-        if (nrec)
-            flush();
+        count = steps - (overrun ? 1u : 0u);
+        if (ns)
+            flush(overrun ? ns - 1 : ns);
         const uint32_t fin = ~crc_small(tab, crc, cert.segment_length, 4);
         if (!(flags & (RAMCRC_SEG_PAST_CAPACITY | RAMCRC_SEG_CYCLE))) {
             if (pos > cert.segment_length)
@@ -1834,6 +1998,28 @@ __global__ __launch_bounds__(256) void k_obj_compare(BatchDesc d, ramcrc_seg_sta
     }
     if (!ok)
         atomicAdd(&status[r.x].bad_objects, 1u);
+}
+
+// Object::assembleForLog (src/Object.cc:213-238): header.checksum =
+// computeChecksum(), i.e. the finalized CRC of bytes [4, len) the scan
+// kernels left in d.out[i], stored little-endian into the object's first 4
+// bytes (which no object's checksum range covers).  Byte stores: objects are
+// packed back to back in a log, so headers are unaligned.
+__global__ __launch_bounds__(256) void k_obj_stamp(BatchDesc d)
+{
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= d.n)
+        return;
+    if (d.len[i] < kObjHeaderBytes) {
+        d.out[i] = 0;
+        return;
+    }
+    const uint32_t c = d.out[i];
+    uint8_t* p = const_cast<uint8_t*>(d.base) + d.off[i];
+    p[0] = uint8_t(c);
+    p[1] = uint8_t(c >> 8);
+    p[2] = uint8_t(c >> 16);
+    p[3] = uint8_t(c >> 24);
 }
 
 }  // namespace
@@ -1920,6 +2106,7 @@ int ramcrc_ctx_destroy(ramcrc_ctx* c)
     if (c->sdesc) (void)hipFree(c->sdesc);
     if (c->sidx) (void)hipFree(c->sidx);
     if (c->sinit) (void)hipFree(c->sinit);
+    if (c->obj_out) (void)hipFree(c->obj_out);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -2030,8 +2217,8 @@ int ramcrc_segments_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_bytes
                                per);
         }
         HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_combine<kSegAligned>, dim3((nseg + 3) / 4), dim3(256), 0, s, d, pl,
-                           per);
+        hipLaunchKernelGGL((k_combine<kSegAligned, false>), dim3((nseg + 3) / 4), dim3(256), 0, s,
+                           d, pl, per);
         HIPCHK(hipGetLastError());
         return RAMCRC_OK;
     }
@@ -2294,6 +2481,77 @@ int ramcrc_verify_objects_device(ramcrc_ctx* c, const void* d_base, uint64_t seg
     const uint64_t grid = (entries_cap + 255) / 256;
     hipLaunchKernelGGL(k_obj_compare, dim3(grid), dim3(256), 0, s, d, d_status);
     HIPCHK(hipGetLastError());
+    return RAMCRC_OK;
+}
+
+int ramcrc_assemble_objects_device(ramcrc_ctx* c, void* d_base, const uint64_t* d_off,
+                                   const uint64_t* d_len, uint32_t* d_out, uint64_t n,
+                                   void* stream)
+{
+    if (n == 0)
+        return c ? RAMCRC_OK : RAMCRC_EINVAL;
+    if (!c || !d_base || !d_off || !d_len)
+        return RAMCRC_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int rc = reserve_locked(c, default_chunk_bound(n), n);
+    if (rc)
+        return rc;
+    if (!d_out) {
+        rc = grow_device(reinterpret_cast<void**>(&c->obj_out), &c->obj_out_cap, n,
+                         sizeof(uint32_t));
+        if (rc)
+            return rc;
+        d_out = c->obj_out;
+    }
+    BatchDesc d{};
+    d.cshift = kChunkShift;
+    d.base = static_cast<const uint8_t*>(d_base);
+    d.off = d_off;
+    d.len = d_len;
+    d.n = n;
+    d.out = d_out;
+    d.flags = RAMCRC_FINALIZE;
+    rc = launch_planned<kObjects>(c, d, s);
+    if (rc)
+        return rc;
+    hipLaunchKernelGGL(k_obj_stamp, dim3((n + 255) / 256), dim3(256), 0, s, d);
+    HIPCHK(hipGetLastError());
+    return RAMCRC_OK;
+}
+
+int ramcrc_assemble_objects_host(ramcrc_ctx* c, void* const* objs, const uint64_t* lens,
+                                 uint64_t n)
+{
+    if (!c || (n && (!objs || !lens)))
+        return RAMCRC_EINVAL;
+    // CRC of bytes [4, len) of every object with a full header through the
+    // pinned-staging batch path, then header.checksum stamped on the host.
+    std::vector<const void*> ptrs;
+    std::vector<uint64_t> ls;
+    std::vector<uint64_t> which;
+    for (uint64_t i = 0; i < n; i++) {
+        if (lens[i] < kObjHeaderBytes)
+            continue;
+        if (!objs[i])
+            return RAMCRC_EINVAL;
+        ptrs.push_back(static_cast<const uint8_t*>(objs[i]) + 4);
+        ls.push_back(lens[i] - 4);
+        which.push_back(i);
+    }
+    if (ptrs.empty())
+        return RAMCRC_OK;
+    std::vector<uint32_t> out(ptrs.size());
+    int rc = ramcrc_batch_host(c, ptrs.data(), ls.data(), nullptr, out.data(), ptrs.size(),
+                               RAMCRC_FINALIZE);
+    if (rc)
+        return rc;
+    for (size_t k = 0; k < which.size(); k++) {
+        uint8_t* p = static_cast<uint8_t*>(objs[which[k]]);
+        for (int b = 0; b < 4; b++)
+            p[b] = uint8_t(out[k] >> (8 * b));
+    }
     return RAMCRC_OK;
 }
 

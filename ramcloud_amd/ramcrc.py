@@ -60,6 +60,8 @@ def lib():
         "ramcrc_segment_walk_device": (i32, [vp, vp, u64, u32, u64, vp, vp, vp, u64, vp, vp]),
         "ramcrc_verify_objects_device": (i32, [vp, vp, u64, vp, u64, vp, vp, vp, vp]),
         "ramcrc_segment_fill_objects": (i32, [vp, u32, u32, u64, _c.POINTER(u32), vp]),
+        "ramcrc_assemble_objects_device": (i32, [vp, vp, vp, vp, vp, u64, vp]),
+        "ramcrc_assemble_objects_host": (i32, [vp, vp, vp, u64]),
         "ramcrc_ctx_set_timing": (i32, [vp, i32]),
         "ramcrc_ctx_scan_time": (i32, [vp, _c.POINTER(_c.c_double), _c.POINTER(u64)]),
         "ramcrc_ctx_status": (i32, [vp, _c.POINTER(u32)]),
@@ -243,6 +245,29 @@ class Context:
                                                 _ptr(status), _stream(stream))
         _check(rc, "ramcrc_verify_objects_device")
         return status
+
+    def assemble_objects(self, data, off, length, out=None, stream=None):
+        """Object::assembleForLog's checksum for serialized objects in `data`
+        (uint8 CUDA tensor, modified in place): header.checksum of object i
+        (bytes [off[i], off[i]+4)) = Crc32C over bytes [4, length[i])."""
+        n = off.numel()
+        rc = lib().ramcrc_assemble_objects_device(self._h, _ptr(data), _ptr(off), _ptr(length),
+                                                  _ptr(out), n, _stream(stream))
+        _check(rc, "ramcrc_assemble_objects_device")
+        return out
+
+    def assemble_objects_host(self, objects):
+        """Same for host objects (writable contiguous numpy uint8 arrays),
+        stamped in place."""
+        for o in objects:
+            if not (isinstance(o, np.ndarray) and o.dtype == np.uint8 and o.flags.c_contiguous
+                    and o.flags.writeable):
+                raise RamcrcError("objects must be writable contiguous numpy uint8 arrays")
+        n = len(objects)
+        ptrs = (_c.c_void_p * max(n, 1))(*[o.ctypes.data for o in objects])
+        lens = np.array([o.size for o in objects], dtype=np.uint64)
+        rc = lib().ramcrc_assemble_objects_host(self._h, ptrs, _c.c_void_p(lens.ctypes.data), n)
+        _check(rc, "ramcrc_assemble_objects_host")
 
     def batch_host(self, buffers, init=None, finalize=True):
         """CRC a list of host buffers (bytes / numpy) on the GPU; returns np.uint32."""

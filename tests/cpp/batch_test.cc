@@ -49,6 +49,26 @@ int main(int argc, char** argv)
                 bad++;
             }
         }
+        // write path: assembleObjects stamps header.checksum = Crc32C over
+        // bytes [4, len) (Object::computeChecksum, src/Object.cc:805-819)
+        std::vector<std::pair<void*, uint64_t> > objs;
+        for (size_t i = 0; i < bufs.size(); i++)
+            objs.push_back(std::make_pair(static_cast<void*>(bufs[i].data()),
+                                          static_cast<uint64_t>(bufs[i].size())));
+        std::vector<std::vector<uint8_t> > before = bufs;
+        batch.assembleObjects(objs);
+        for (size_t i = 0; i < bufs.size(); i++) {
+            std::vector<uint8_t> want = before[i];
+            if (want.size() >= 24) {
+                const uint32_t c = Crc32C().update(&want[4],
+                                                   static_cast<uint32_t>(want.size() - 4)).getResult();
+                memcpy(&want[0], &c, 4);
+            }
+            if (want != bufs[i]) {
+                fprintf(stderr, "object %zu (%zu B): header checksum mismatch\n", i, want.size());
+                bad++;
+            }
+        }
         printf("gpu batch: %zu buffers, %d mismatches\n", bufs.size(), bad);
         return bad ? 1 : 0;
     } catch (const std::runtime_error& e) {

@@ -4,7 +4,7 @@ Every expected value in the fixture comes from the reference itself:
   * `crc32c_test` -- the input array and 82 CRCs held by the reference's own
     unit test, src/Crc32CTest.cc:27-58 (parsed from the file as data);
   * `segment_certificates` / `object_checksums` -- the golden constants held by
-    src/SegmentTest.cc:159,369,373 and src/ObjectTest.cc:171, with the byte
+    src/SegmentTest.cc:159,369,373 and src/ObjectTest.cc:171,321,913, with the byte
     strings those tests checksum, rebuilt from the formats in src/Segment.cc:197-228,
     :672-684 (EntryHeader + length bytes + SegmentCertificate.segmentLength)
     and src/Object.cc:770-819 (header bytes [4,24) + keysAndValue);
@@ -94,8 +94,23 @@ def main():
     hdr = struct.pack("<IQQ", 723, 75, 57)
     kv = bytes([3]) + struct.pack("<HHH", 3, 6, 9) + b"ha\0hi\0ho\0" + b"YO!\0"
     assert ref_result(hdr + kv) == 0xBB68333C
+    # single-key object (src/ObjectTest.cc:117 fixture, golden :321): key "ha\0"
+    # of table 57, value "YO!\0", version 75, timestamp 723
+    kv1 = bytes([1]) + struct.pack("<H", 3) + b"ha\0" + b"YO!\0"
+    assert ref_result(hdr + kv1) == 0xE86291D1
     out["object_checksums"] = [{"bytes": (hdr + kv).hex(), "checksum": 0xBB68333C,
-                                "cite": "src/ObjectTest.cc:171"}]
+                                "cite": "src/ObjectTest.cc:171"},
+                               {"bytes": (hdr + kv1).hex(), "checksum": 0xE86291D1,
+                                "cite": "src/ObjectTest.cc:321"}]
+    # ObjectTombstone::computeChecksum (src/Object.cc:1042-1057): header bytes
+    # before the trailing checksum {tableId u64, segmentId u64, objectVersion
+    # u64, timestamp u32} (src/Object.h:301-336), then the key; fixture
+    # src/ObjectTest.cc:843-866 (key "key!\0", table 572, segment 925, version
+    # 58, timestamp 335), golden :913
+    tomb = struct.pack("<QQQI", 572, 925, 58, 335) + b"key!\0"
+    assert ref_result(tomb) == 0x5D60E8EF
+    out["tombstone_checksums"] = [{"bytes": tomb.hex(), "checksum": 0x5D60E8EF,
+                                   "cite": "src/ObjectTest.cc:913"}]
 
     kats = []
     for name, data in (("zeros_8MiB", np.zeros(8 * MiB, np.uint8)),

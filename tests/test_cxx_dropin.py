@@ -14,7 +14,7 @@ def test_cxx_dropin(golden, ramcrc, tmp_path):
         f.write("INPUT " + bytes(golden["crc32c_test"]["input"]).hex() + "\n")
         for c in golden["crc32c_test"]["crcByLength"]:
             f.write(f"CRC {c:08x}\n")
-        for c in golden["segment_certificates"] + golden["object_checksums"]:
+        for c in golden["segment_certificates"] + golden["object_checksums"] + golden["tombstone_checksums"]:
             data = c.get("stream", c.get("bytes"))
             f.write(f"GOLDEN {data} {c['checksum']:08x}\n")
     exe = tmp_path / "crc32c_test"

@@ -91,8 +91,8 @@ def test_crc32c_test_accumulated_chain(ctx, golden):
 
 def test_segment_and_object_goldens(ctx, golden):
     items = [bytes.fromhex(c.get("stream", c.get("bytes")))
-             for c in golden["segment_certificates"] + golden["object_checksums"]]
-    want = [c["checksum"] for c in golden["segment_certificates"] + golden["object_checksums"]]
+             for c in golden["segment_certificates"] + golden["object_checksums"] + golden["tombstone_checksums"]]
+    want = [c["checksum"] for c in golden["segment_certificates"] + golden["object_checksums"] + golden["tombstone_checksums"]]
     blob = b"".join(items)
     off = np.cumsum([0] + [len(x) for x in items[:-1]])
     got = run_api(ctx, "batch", dev(np.frombuffer(blob, np.uint8)), off, [len(x) for x in items],
@@ -168,6 +168,29 @@ def test_batch_mixed_lengths_and_overlaps(ctx, oracle_mod):
     # default init
     got = run_api(ctx, "batch", base, offs, lens, None, True)
     assert np.array_equal(got, oracle_mod.entries(host, offs, lens))
+
+
+@pytest.mark.parametrize("api", ["entries", "batch"])
+def test_entries_every_alignment(ctx, oracle_mod, api):
+    """Every start offset within a 128-byte line x every length up to three
+    windows (plus a few longer): the small-entry kernels' window geometry
+    (one window, entry ending exactly at a window end, init bytes crossing a
+    line) is exercised at each alignment."""
+    host = oracle_mod.splitmix_bytes(4242, 1 << 20)
+    lens = list(range(0, 400)) + [511, 512, 513, 1023, 1024, 1025, 4095, 4096, 4097]
+    offs, ls = [], []
+    for s in range(128):
+        for L in lens:
+            offs.append(1024 + s + 128 * ((s * 7 + L) % 64))
+            ls.append(L)
+    rng = np.random.default_rng(77)
+    init = rng.integers(0, 2 ** 32, len(offs), dtype=np.uint64).astype(np.uint32)
+    base = dev(host)
+    for it in (None, init):
+        got = run_api(ctx, api, base, offs, ls, it, True)
+        want = oracle_mod.entries(host, offs, ls, init=it)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, [(offs[i] % 128, ls[i]) for i in bad[:8]]
 
 
 def test_entries_config3_sample(ctx, oracle_mod):

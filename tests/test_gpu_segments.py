@@ -64,6 +64,33 @@ def test_walk_verify_clean_1mib(ramcrc, oracle_mod):
 
 
 @pytest.mark.gpu
+def test_walk_verify_strided_high_addresses(ramcrc, oracle_mod):
+    """Segments spread over 4.5 GiB of device memory (stride 72 MiB): window
+    and object addresses whose low 32 bits have bit 31 set, or that cross a
+    4 GiB boundary, must be formed correctly (64-bit scalar addresses)."""
+    import torch
+
+    cap, nseg, stride = 256 * 1024, 64, 72 << 20
+    buf, certs, counts = segments.object_segments_host(nseg, cap, 1000)
+    d = torch.zeros(nseg * stride, dtype=torch.uint8, device="cuda")
+    for i in range(nseg):
+        d[i * stride:i * stride + cap].copy_(torch.from_numpy(buf[i * cap:(i + 1) * cap]))
+    ctx = ramcrc.Context(0)
+    dc = torch.from_numpy(np.ascontiguousarray(certs).view(np.int32)).cuda()
+    rv = segments.RecoveryVerify(ctx, nseg, cap, stride=stride, entries_cap=int(counts.sum()) + 1)
+    st = rv.verify(d, dc)
+    torch.cuda.synchronize()
+    status = st.cpu().numpy().view(np.uint32)
+    assert (status[:, 0] == segments.SEG_OK).all()
+    assert (status[:, 3] == 0).all()
+    assert np.array_equal(status[:, 2], counts)
+    n = int(rv.n_entries.item())
+    table = rv.entries[:n].cpu().numpy().view(np.uint32)
+    _, crc_exp, _ = oracle_mod.verify_objects(buf, cap, table, nseg)
+    assert np.array_equal(rv.obj_crc[:n].cpu().numpy().view(np.uint32), crc_exp)
+
+
+@pytest.mark.gpu
 def test_walk_table_full_flag(ramcrc, oracle_mod):
     """A table too small for the walk: records dropped, flagged, count still exact."""
     cap, nseg = 1 << 18, 4

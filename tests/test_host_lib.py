@@ -32,7 +32,7 @@ def test_host_known_answers(golden, ramcrc, path):
     inp = bytes(golden["crc32c_test"]["input"])
     for i, want in enumerate(golden["crc32c_test"]["crcByLength"]):
         assert (~f(0xFFFFFFFF, inp[:i])) & 0xFFFFFFFF == want
-    for c in golden["segment_certificates"] + golden["object_checksums"]:
+    for c in golden["segment_certificates"] + golden["object_checksums"] + golden["tombstone_checksums"]:
         data = bytes.fromhex(c.get("stream", c.get("bytes")))
         assert (~f(0xFFFFFFFF, data)) & 0xFFFFFFFF == c["checksum"]
 

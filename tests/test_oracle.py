@@ -31,7 +31,7 @@ def test_crc32c_test_accumulated(golden, oracle_mod, impl):
 
 @pytest.mark.parametrize("impl", IMPLS)
 def test_segment_and_object_goldens(golden, oracle_mod, impl):
-    for c in golden["segment_certificates"] + golden["object_checksums"]:
+    for c in golden["segment_certificates"] + golden["object_checksums"] + golden["tombstone_checksums"]:
         data = bytes.fromhex(c.get("stream", c.get("bytes")))
         assert oracle_mod.crc32c(data, impl) == c["checksum"], c["cite"]
 
