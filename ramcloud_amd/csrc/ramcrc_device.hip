@@ -1913,10 +1913,13 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
             const uint64_t wend = uint64_t(wb) + (kWalkWin - 8);
             const uint32_t last = limit - 1 < wend ? limit - 1 : uint32_t(wend);
             const uint32_t span = last - wb;
-            uint32_t room = uint32_t(kWaveSize) - ns;
-            if (cap32 - steps < room)
-                room = cap32 - steps;
-            for (uint32_t k = 0; k < room; k++) {
+            // the batch and the cycle bound: at most nsmax - ns hops
+            uint32_t nsmax = uint32_t(kWaveSize);
+            if (cap32 - steps < nsmax - ns)
+                nsmax = ns + (cap32 - steps);
+            const uint32_t ns0 = ns;
+            uint32_t next;
+            for (;;) {
                 const uint32_t o = pos - wb;
                 const uint32_t d0 = __builtin_amdgcn_readfirstlane(w32[o >> 2]);
                 const uint32_t d1 = __builtin_amdgcn_readfirstlane(w32[(o >> 2) + 1]);
@@ -1929,30 +1932,34 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
                 // A payload past the capacity is only reachable through the
                 // wrap (carry out of 32 bits): flagged unreadable.
                 const uint32_t hl = pos + 1 + lb;
-                uint32_t next, ovl;
+                uint32_t ovl;
                 // scalar add with carry (the compiler would route the carry
                 // through a VALU add and back)
                 asm("s_add_u32 %0, %2, %3\n\ts_cselect_b32 %1, 0x100, 0"
                     : "=s"(next), "=s"(ovl) : "s"(hl), "s"(len) : "scc");
                 const uint32_t info = hdr | ovl;   // kRecOverlong
-                const bool mine = lane == int(ns);   // park: one compare, three selects
+                // park in lane ns (one compare, three selects)
+                const bool mine = lane == int(ns);
                 rpos = mine ? pos : rpos;
                 rlen = mine ? len : rlen;
                 rinfo = mine ? info : rinfo;
                 ns++;
-                steps++;
-                if (next > cap32) {
-                    // its header and length were checksummed; it is not a record
-                    flags |= RAMCRC_SEG_PAST_CAPACITY;
-                    overrun = true;
+                // one exit test: the next header leaves the window or the
+                // limit (which also covers next > capacity and a wrapped
+                // next), or the batch is full
+                if (next - wb > span || ns == nsmax)
                     break;
-                }
                 pos = next;
-                if (pos - wb > span)
-                    break;
             }
-            if (overrun)
+            steps += ns - ns0;
+            if (next > cap32) {
+                // the last hop's header and length were checksummed; that
+                // entry is not a record
+                flags |= RAMCRC_SEG_PAST_CAPACITY;
+                overrun = true;
                 break;
+            }
+            pos = next;
         }
         count = steps - (overrun ? 1u : 0u);
         if (ns)
