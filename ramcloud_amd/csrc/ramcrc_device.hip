@@ -1823,16 +1823,27 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
         const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
         const ramcrc_seg_cert cert = w.certs[seg];
         uint32_t pos = 0, crc = 0xFFFFFFFFu, count = 0, flags = 0;
-        // Parked entries: lane j holds entry j of the current batch of 64.
-        uint32_t rpos = 0, rlen = 0, rinfo = 0;
+        // Parked entries: lane j holds entry j of the current batch of 64 --
+        // its offset and the 4 bytes from its header on.  Its length is
+        // recovered at the flush from the offset of the entry after it
+        // (len = next - pos - 1 - lengthBytes, mod 2^32), so a hop parks two
+        // values, not four.
+        uint32_t rpos = 0, rq = 0;
         uint32_t ns = 0;
 
         // Fold the parked entries' header + length bytes into crc and append
         // the first nrec of them to the record table.
-        auto flush = [&](uint32_t nrec) {
+        // tail: the offset after the last parked entry (its `next`).
+        auto flush = [&](uint32_t nrec, uint32_t tail) {
+            const uint32_t pn = __shfl_down(rpos, 1, kWaveSize);
+            const uint32_t nxt = lane + 1 == int(ns) ? tail : pn;
+            const uint32_t hdr = rq & 0xFF, lb = (hdr >> 6) + 1;
+            const uint32_t rlen = nxt - rpos - 1 - lb;
+            // a payload past 2^32 (carry out of the reference's uint32_t
+            // offset) is unreadable: kRecOverlong
+            const uint32_t rinfo = hdr | (rlen > ~(rpos + 1 + lb) ? kRecOverlong : 0u);
             uint32_t m = 0, r = 0;
             if (lane < int(ns)) {
-                const uint32_t hdr = rinfo & 0xFF, lb = (hdr >> 6) + 1;
                 m = 1 + lb;
                 r = crc_small(tab, 0u, hdr | (rlen << 8), m < 4 ? m : 4);
                 if (m == 5)
@@ -1882,7 +1893,7 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
         // the window, the batch has room and the cycle bound is not reached.
         const uint32_t cap32 = uint32_t(w.capacity);
         const uint32_t limit = cert.segment_length < cap32 ? cert.segment_length : cap32;
-        uint32_t steps = 0;
+        uint32_t steps = 0, tail = 0;
         bool overrun = false;
         while (pos < limit) {
             // deterministic walk below the capacity: more steps than bytes means
@@ -1906,7 +1917,7 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
                 walk_issue(pf, sb, uint64_t(wb) + kWalkStep, w.capacity, lane);
             }
             if (ns == uint32_t(kWaveSize))
-                flush(ns);
+                flush(ns, pos);
             const uint32_t* w32 = reinterpret_cast<const uint32_t*>(win[cur]);
             // hop while pos - wb <= span (header + 7 bytes inside the window, pos
             // below the limit) and the batch and the cycle bound have room
@@ -1924,34 +1935,29 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
                 const uint32_t d0 = __builtin_amdgcn_readfirstlane(w32[o >> 2]);
                 const uint32_t d1 = __builtin_amdgcn_readfirstlane(w32[(o >> 2) + 1]);
                 const uint64_t q = ((uint64_t(d1) << 32) | d0) >> (8 * (o & 3));
-                const uint32_t hdr = uint32_t(q) & 0xFF;
-                const uint32_t lb = (hdr >> 6) + 1;                       // getLengthBytes()
-                const uint32_t len = uint32_t(q >> 8) & (0xFFFFFFFFu >> (32 - 8 * lb));
-                // next = pos + 1 + lb + len in uint32_t arithmetic, as the
-                // reference; pos + 1 + lb cannot wrap (pos < capacity < 2^32 - 16).
-                // A payload past the capacity is only reachable through the
-                // wrap (carry out of 32 bits): flagged unreadable.
-                const uint32_t hl = pos + 1 + lb;
-                uint32_t ovl;
-                // scalar add with carry (the compiler would route the carry
-                // through a VALU add and back)
-                asm("s_add_u32 %0, %2, %3\n\ts_cselect_b32 %1, 0x100, 0"
-                    : "=s"(next), "=s"(ovl) : "s"(hl), "s"(len) : "scc");
-                const uint32_t info = hdr | ovl;   // kRecOverlong
-                // park in lane ns (one compare, three selects)
-                const bool mine = lane == int(ns);
+                const uint32_t t = (uint32_t(q) >> 6) & 3;   // getLengthBytes() - 1
+                // len = the t + 1 bytes after the header: one s_bfe_u64, field
+                // {offset 8, width 8 t + 8}
+                uint32_t fld;
+                uint64_t len64;
+                asm("s_lshl_b32 %0, %2, 19\n\ts_add_u32 %0, %0, 0x80008\n\ts_bfe_u64 %1, %3, %0"
+                    : "=&s"(fld), "=s"(len64) : "s"(t), "s"(q) : "scc");
+                // uint32_t arithmetic, as the reference (a wrap is legal)
+                next = pos + t + 2 + uint32_t(len64);
+                const bool mine = lane == int(ns);   // park: one compare, two selects
                 rpos = mine ? pos : rpos;
-                rlen = mine ? len : rlen;
-                rinfo = mine ? info : rinfo;
+                rq = mine ? uint32_t(q) : rq;
                 ns++;
-                // one exit test: the next header leaves the window or the
-                // limit (which also covers next > capacity and a wrapped
-                // next), or the batch is full
-                if (next - wb > span || ns == nsmax)
+                // the next header leaves the window or the limit (this also
+                // covers next > capacity and a wrapped next)
+                if (next - wb > span)
+                    break;
+                if (ns == nsmax)   // the batch is full, or the cycle bound
                     break;
                 pos = next;
             }
             steps += ns - ns0;
+            tail = next;
             if (next > cap32) {
                 // the last hop's header and length were checksummed; that
                 // entry is not a record
@@ -1963,7 +1969,7 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
         }
         count = steps - (overrun ? 1u : 0u);
         if (ns)
-            flush(overrun ? ns - 1 : ns);
+            flush(overrun ? ns - 1 : ns, tail);
         const uint32_t fin = ~crc_small(tab, crc, cert.segment_length, 4);
         if (!(flags & (RAMCRC_SEG_PAST_CAPACITY | RAMCRC_SEG_CYCLE))) {
             if (pos > cert.segment_length)
