@@ -1149,26 +1149,14 @@ __global__ __launch_bounds__(kThreads, 1) void k_entries_tiny(BatchDesc d, Sorte
 // kSmallK+1 and up.  Two instantiations keep the register allocation of the
 // long-entry loop free of the short-entry loop's state.
 template <bool kSmall>
-__global__ __launch_bounds__(kThreads, 1) void k_entries(BatchDesc d, Sorted so)
+__device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so, const uint8_t* lds)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsEntries];
     constexpr int b0 = kSmall ? 2 : kSmallK + 1, b1 = kSmall ? kSmallK + 1 : kNB;
-    if (so.bt->items[b0] == so.bt->items[b1])
-        return;   // no entry in this kernel's bins
-    fill_replicated(lds, g_tab.stride_small);
-    fill_plain(lds, kX4Off, &g_tab.comb[0].t[0][0], 4 * 1024);
-    fill_plain(lds, kXinvOff, g_tab.xinv, 128);
-    uint64_t* s_items = reinterpret_cast<uint64_t*>(lds + kBinOff);   // kNB + 1
-    uint64_t* s_start = s_items + (kNB + 1);                          // kNB
-    uint32_t* s_cost = reinterpret_cast<uint32_t*>(s_start + kNB);    // kNB
-    for (int t = threadIdx.x; t <= kNB; t += blockDim.x) {
-        s_items[t] = so.bt->items[t];
-        if (t < kNB) {
-            s_start[t] = so.bt->start[t];
-            s_cost[t] = uint32_t(so.bt->kcost[t]);
-        }
-    }
-    __syncthreads();
+    const uint64_t* s_items = reinterpret_cast<const uint64_t*>(lds + kBinOff);   // kNB + 1
+    const uint64_t* s_start = s_items + (kNB + 1);                                // kNB
+    const uint32_t* s_cost = reinterpret_cast<const uint32_t*>(s_start + kNB);    // kNB
+    if (s_items[b0] == s_items[b1])
+        return;   // no entry in this phase's bins (uniform)
     const uint32_t* xinv = reinterpret_cast<const uint32_t*>(lds + kXinvOff);
 
     const int lane = threadIdx.x & (kWaveSize - 1);
@@ -1432,6 +1420,32 @@ __global__ __launch_bounds__(kThreads, 1) void k_entries(BatchDesc d, Sorted so)
     flush();
     if (nb)
         flush_batch();
+}
+
+// Both phases in one launch (one LDS fill, one launch boundary): the exact
+// short bins, then the pipelined long bins.  The phases are separate inlined
+// loops, so the long-entry loop's registers are not shared with the short one.
+__global__ __launch_bounds__(kThreads, 1) void k_entries(BatchDesc d, Sorted so)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsEntries];
+    if (so.bt->items[2] == so.bt->items[kNB])
+        return;   // every entry is tiny (or large on the batch path)
+    fill_replicated(lds, g_tab.stride_small);
+    fill_plain(lds, kX4Off, &g_tab.comb[0].t[0][0], 4 * 1024);
+    fill_plain(lds, kXinvOff, g_tab.xinv, 128);
+    uint64_t* s_items = reinterpret_cast<uint64_t*>(lds + kBinOff);   // kNB + 1
+    uint64_t* s_start = s_items + (kNB + 1);                          // kNB
+    uint32_t* s_cost = reinterpret_cast<uint32_t*>(s_start + kNB);    // kNB
+    for (int t = threadIdx.x; t <= kNB; t += blockDim.x) {
+        s_items[t] = so.bt->items[t];
+        if (t < kNB) {
+            s_start[t] = so.bt->start[t];
+            s_cost[t] = uint32_t(so.bt->kcost[t]);
+        }
+    }
+    __syncthreads();
+    entries_run<true>(d, so, lds);
+    entries_run<false>(d, so, lds);
 }
 
 // ------------------------------------------------------------ k_plan
@@ -1704,8 +1718,7 @@ int launch_binned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_lar
     {
         ScanTimer t(c, s);
         hipLaunchKernelGGL(k_entries_tiny, dim3(c->ncu), dim3(kThreads), 0, s, d, so);
-        hipLaunchKernelGGL(k_entries<true>, dim3(c->ncu), dim3(kThreads), 0, s, d, so);
-        hipLaunchKernelGGL(k_entries<false>, dim3(c->ncu), dim3(kThreads), 0, s, d, so);
+        hipLaunchKernelGGL(k_entries, dim3(c->ncu), dim3(kThreads), 0, s, d, so);
     }
     HIPCHK(hipGetLastError());
     return RAMCRC_OK;

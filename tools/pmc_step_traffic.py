@@ -2,7 +2,7 @@
 profiles/pmc_summary.json.
 
 A step of the entries path is several launches (binning + k_entries_tiny +
-k_entries<true> + k_entries<false>); this sums FETCH_SIZE per launch over the
+k_entries); this sums FETCH_SIZE per launch over the
 named scan kernels. Same correction as tools/pmc_summary.py:
 FETCH_SIZE (KiB) x 1024 x 2 (MI355X_MICROARCH.md, HBM section).
 usage: python tools/pmc_step_traffic.py <pmc csv> <key> <kernel substring>...

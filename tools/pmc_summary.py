@@ -10,7 +10,7 @@ import csv
 import json
 import sys
 
-KERNELS = {"k_chunks": "k_chunks<", "k_combine": "k_combine<", "k_entries": "k_entries<",
+KERNELS = {"k_chunks": "k_chunks<", "k_combine": "k_combine<", "k_entries": "k_entries((",
            "k_plan_count": "k_plan_count", "k_plan_scan": "k_plan_scan"}
 
 
