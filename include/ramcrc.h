@@ -149,7 +149,8 @@ typedef struct ramcrc_seg_status {
     uint32_t flags;        /* RAMCRC_SEG_* */
     uint32_t checksum;     /* metadata checksum the walk computed (over the entries walked + length) */
     uint32_t entries;      /* entries walked */
-    uint32_t bad_objects;  /* objects whose Object::Header::checksum did not match */
+    uint32_t bad_objects;  /* replay records whose checksum check failed: objects, tombstones
+                              and safe versions (see ramcrc_verify_objects_device) */
 } ramcrc_seg_status;
 
 #define RAMCRC_SEG_OK 1u              /* Segment::checkMetadataIntegrity returned true */
@@ -159,7 +160,9 @@ typedef struct ramcrc_seg_status {
 #define RAMCRC_SEG_TABLE_FULL 16u     /* entry table capacity exhausted: records dropped */
 #define RAMCRC_SEG_CYCLE 32u          /* the walk revisited an offset (uint32_t wrap): the
                                          reference's loop would not terminate; stopped */
-#define RAMCRC_LOG_ENTRY_TYPE_OBJ 2u  /* LOG_ENTRY_TYPE_OBJ, src/LogEntryTypes.h:35 */
+#define RAMCRC_LOG_ENTRY_TYPE_OBJ 2u          /* LOG_ENTRY_TYPE_OBJ, src/LogEntryTypes.h:35 */
+#define RAMCRC_LOG_ENTRY_TYPE_OBJTOMB 3u      /* LOG_ENTRY_TYPE_OBJTOMB, src/LogEntryTypes.h:38 */
+#define RAMCRC_LOG_ENTRY_TYPE_SAFEVERSION 5u  /* LOG_ENTRY_TYPE_SAFEVERSION, src/LogEntryTypes.h:44 */
 
 /* Segment::checkMetadataIntegrity (src/Segment.cc:758-800) for n_seg segments
  * at d_base + i*seg_stride, each of seg_capacity bytes (a multiple of 16; the
@@ -176,17 +179,25 @@ int ramcrc_segment_walk_device(ramcrc_ctx* ctx, const void* d_base, uint64_t seg
                                ramcrc_seg_entry* d_entries, uint64_t entries_cap,
                                uint64_t* d_n_entries, void* stream);
 
-/* Object::computeChecksum (src/Object.cc:805-819) for every LOG_ENTRY_TYPE_OBJ
- * record of a walk whose segment passed the metadata check (d_status flags
- * RAMCRC_SEG_OK; records of failed segments are skipped, as
- * RecoverySegmentBuilder::build stops there), compared with the object's
- * stored checksum as ObjectManager::replaySegment does
- * (src/ObjectManager.cc:659-669): CRC32C over payload bytes [4, length) into
- * d_obj_crc[i] (other records: not written), and
- * d_status[segment].bad_objects += 1 per mismatch (objects shorter than their
- * 24-byte header or flagged OVERLONG count as mismatches).  Objects of
- * >= 64 KiB are scanned by all CUs, smaller ones by the small-entry kernels.
- * Stream-ordered after the walk that produced the table. */
+/* ObjectManager::replaySegment's checksum checks for every record of a walk
+ * whose segment passed the metadata check (d_status flags RAMCRC_SEG_OK;
+ * records of failed segments are skipped, as RecoverySegmentBuilder::build
+ * stops there):
+ *   LOG_ENTRY_TYPE_OBJ          Object::computeChecksum (src/Object.cc:805-819)
+ *                               over payload bytes [4, length) vs. the stored
+ *                               checksum at [0, 4) (src/ObjectManager.cc:659-669);
+ *   LOG_ENTRY_TYPE_OBJTOMB      ObjectTombstone::checkIntegrity
+ *                               (src/ObjectManager.cc:752-758): bytes [0, 28) and
+ *                               the key [32, length) vs. the checksum at [28, 32);
+ *   LOG_ENTRY_TYPE_SAFEVERSION  ObjectSafeVersion::checkIntegrity
+ *                               (src/ObjectManager.cc:873-880): bytes [0, 8) vs.
+ *                               the checksum at [8, 12).
+ * The computed CRC goes to d_obj_crc[i] (other records: not written), and
+ * d_status[segment].bad_objects += 1 per failed check (records shorter than
+ * their type's header, 24 / 32 / 12 bytes, or flagged OVERLONG fail).  Objects
+ * of >= 64 KiB are scanned by all CUs, smaller ones by the small-entry
+ * kernels; tombstones and safe versions by one thread each.  Stream-ordered
+ * after the walk that produced the table. */
 int ramcrc_verify_objects_device(ramcrc_ctx* ctx, const void* d_base, uint64_t seg_stride,
                                  const ramcrc_seg_entry* d_entries, uint64_t entries_cap,
                                  const uint64_t* d_n_entries, uint32_t* d_obj_crc,

@@ -407,32 +407,57 @@ uint32_t oracle_check_metadata(const uint8_t* seg, uint64_t capacity, uint32_t c
     return flags;
 }
 
-/* Object::computeChecksum of every OBJ record (4 uint32 each) of segments at
- * base + segment*stride whose metadata check passed (seg_ok[segment] != 0, or
- * every segment when seg_ok is NULL) -- RecoverySegmentBuilder::build stops at
- * a failed check (src/RecoverySegmentBuilder.cc:61-203), so nothing of such a
- * segment is replayed.  crc_out[i] for readable objects of >= 24 bytes;
- * returns the number of mismatches (short or unreadable objects count as
- * mismatches) and adds them to bad_per_seg[segment] when that is non-NULL. */
+/* The checksum checks ObjectManager::replaySegment makes on the records (4
+ * uint32 each) of segments at base + segment*stride whose metadata check
+ * passed (seg_ok[segment] != 0, or every segment when seg_ok is NULL) --
+ * RecoverySegmentBuilder::build stops at a failed check
+ * (src/RecoverySegmentBuilder.cc:61-203), so nothing of such a segment is
+ * replayed:
+ *   OBJ (2)          Object::computeChecksum (src/Object.cc:805-819): bytes
+ *                    [4, len) against the stored header.checksum at [0, 4)
+ *                    (src/ObjectManager.cc:659-663);
+ *   OBJTOMB (3)      ObjectTombstone::computeChecksum (src/Object.cc:1042-1057):
+ *                    header bytes [0, 28) then the key [32, len), against
+ *                    header.checksum at [28, 32) (src/ObjectManager.cc:752-758);
+ *   SAFEVERSION (5)  ObjectSafeVersion::computeChecksum (src/Object.cc:1135-1143):
+ *                    bytes [0, 8) against header.checksum at [8, 12)
+ *                    (src/ObjectManager.cc:873-880).
+ * crc_out[i] receives the computed CRC of each readable record of these types
+ * that holds at least its header (24, 32, 12 bytes).  Returns the number of
+ * failed checks; shorter or unreadable records count as failures (the
+ * reference would read past the entry there).  Failures are added to
+ * bad_per_seg[segment] when that is non-NULL. */
 uint64_t oracle_verify_objects(const uint8_t* base, uint64_t stride, const uint32_t* table,
                                uint64_t n, const uint8_t* seg_ok, uint32_t* crc_out,
                                uint32_t* bad_per_seg)
 {
+    /* Crc32C picks the crc32 instruction when the CPU has it
+     * (src/Crc32C.h:200-206); both forms agree bit for bit */
+    const crc_fn f = oracle_have_sse42() ? oracle_sse42 : oracle_slicing8;
     uint64_t bad = 0;
     for (uint64_t i = 0; i < n; i++) {
         const uint32_t* r = table + 4 * i;
-        if ((r[3] & 0x3f) != 2 || (seg_ok && !seg_ok[r[0]]))
+        const uint32_t type = r[3] & 0x3f;
+        if ((type != 2 && type != 3 && type != 5) || (seg_ok && !seg_ok[r[0]]))
             continue;
+        const uint32_t hdr = type == 2 ? 24u : type == 3 ? 32u : 12u;
         int ok = 0;
-        if (r[2] >= 24 && !(r[3] & 0x100)) {
+        if (r[2] >= hdr && !(r[3] & 0x100)) {
             const uint8_t* payload = base + (uint64_t)r[0] * stride + r[1] + 1 + ((r[3] >> 6) & 3) + 1;
-            /* Crc32C picks the crc32 instruction when the CPU has it
-             * (src/Crc32C.h:200-206); both forms agree bit for bit */
-            const crc_fn f = oracle_have_sse42() ? oracle_sse42 : oracle_slicing8;
-            uint32_t c = ~f(0xFFFFFFFFu, payload + 4, r[2] - 4);
+            uint32_t c, stored;
+            if (type == 2) {
+                c = ~f(0xFFFFFFFFu, payload + 4, r[2] - 4);
+                stored = oracle_u32le(payload);
+            } else if (type == 3) {
+                c = ~f(f(0xFFFFFFFFu, payload, 28), payload + 32, r[2] - 32);
+                stored = oracle_u32le(payload + 28);
+            } else {
+                c = ~f(0xFFFFFFFFu, payload, 8);
+                stored = oracle_u32le(payload + 8);
+            }
             if (crc_out)
                 crc_out[i] = c;
-            ok = c == oracle_u32le(payload);
+            ok = c == stored;
         }
         if (!ok) {
             bad++;

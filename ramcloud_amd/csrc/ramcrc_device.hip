@@ -366,7 +366,9 @@ struct BatchDesc {
 //                shorter than their 24-byte header are inactive.
 enum Mode { kSegAligned = 0, kSegUniform = 1, kTable = 2, kRecords = 3, kObjects = 4 };
 
-constexpr uint32_t kObjHeaderBytes = 24;   // Object::Header, src/Object.h:137-182
+constexpr uint32_t kObjHeaderBytes = 24;     // Object::Header, src/Object.h:137-182
+constexpr uint32_t kTombHeaderBytes = 32;    // ObjectTombstone::Header, src/Object.h:285-338
+constexpr uint32_t kSafeVersionBytes = 12;   // ObjectSafeVersion::Header, src/Object.h:402-427
 constexpr uint32_t kRecOverlong = 0x100;   // record header bit: payload past the capacity
 
 template <int kMode>
@@ -2003,24 +2005,63 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
     }
 }
 
-// ObjectManager::replaySegment's comparison (src/ObjectManager.cc:659-669):
-// computed object CRC vs. Object::Header::checksum (the payload's first 4 B).
+// ObjectManager::replaySegment's checksum checks on the walk records of the
+// segments that passed the metadata check:
+//   OBJ          computed object CRC (left in d.out[i] by the scan kernels) vs.
+//                Object::Header::checksum, the payload's first 4 B
+//                (src/ObjectManager.cc:659-669);
+//   OBJTOMB      ObjectTombstone::checkIntegrity (src/ObjectManager.cc:752-758,
+//                src/Object.cc:1014-1057): CRC of header bytes [0, 28) and the
+//                key [32, len) vs. the checksum at [28, 32);
+//   SAFEVERSION  ObjectSafeVersion::checkIntegrity (src/ObjectManager.cc:873-880,
+//                src/Object.cc:1107-1143): CRC of [0, 8) vs. the checksum at [8, 12).
+// Tombstones and safe versions are rare and short (a key), so one thread runs
+// the byte-table CRC over each and writes it to d.out[i].  Records shorter
+// than their type's header, or unreadable, count as failures.
+__device__ __forceinline__ uint32_t crc_bytes_g(const uint32_t* t1, uint32_t c, const gu8* p,
+                                                uint32_t n)
+{
+    for (uint32_t k = 0; k < n; k++)
+        c = t1[(c ^ p[k]) & 0xFF] ^ (c >> 8);
+    return c;
+}
+
+__device__ __forceinline__ uint32_t le32_g(const gu8* p)
+{
+    return uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
+}
+
 __global__ __launch_bounds__(256) void k_obj_compare(BatchDesc d, ramcrc_seg_status* status)
 {
     const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= entry_count<kRecords>(d))
         return;
     const u32x4 r = d.rec[i];
-    if ((r.w & 0x3f) != RAMCRC_LOG_ENTRY_TYPE_OBJ || !(d.seg_status[r.x].x & RAMCRC_SEG_OK))
+    const uint32_t type = r.w & 0x3f;
+    if ((type != RAMCRC_LOG_ENTRY_TYPE_OBJ && type != RAMCRC_LOG_ENTRY_TYPE_OBJTOMB &&
+         type != RAMCRC_LOG_ENTRY_TYPE_SAFEVERSION) ||
+        !(d.seg_status[r.x].x & RAMCRC_SEG_OK))
         return;
+    const uint32_t hdr = type == RAMCRC_LOG_ENTRY_TYPE_OBJ ? kObjHeaderBytes
+                         : type == RAMCRC_LOG_ENTRY_TYPE_OBJTOMB ? kTombHeaderBytes
+                                                                 : kSafeVersionBytes;
     bool ok = false;
-    if (r.z >= kObjHeaderBytes && !(r.w & kRecOverlong)) {
+    if (r.z >= hdr && !(r.w & kRecOverlong)) {
         const uint64_t payload = reinterpret_cast<uint64_t>(d.base) + uint64_t(r.x) * d.seg_bytes +
                                  r.y + 1 + ((r.w >> 6) & 3) + 1;
         const gu8* p = reinterpret_cast<const gu8*>(payload);
-        const uint32_t stored = uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) |
-                                (uint32_t(p[3]) << 24);
-        ok = d.out[i] == stored;
+        if (type == RAMCRC_LOG_ENTRY_TYPE_OBJ) {
+            ok = d.out[i] == le32_g(p);
+        } else {
+            const uint32_t* t1 = &g_tab.pos[1 + kTinyRow0][0];   // X^1(b): the byte step
+            uint32_t c;
+            if (type == RAMCRC_LOG_ENTRY_TYPE_OBJTOMB)
+                c = ~crc_bytes_g(t1, crc_bytes_g(t1, 0xFFFFFFFFu, p, 28), p + 32, r.z - 32);
+            else
+                c = ~crc_bytes_g(t1, 0xFFFFFFFFu, p, 8);
+            d.out[i] = c;
+            ok = c == le32_g(p + hdr - 4);
+        }
     }
     if (!ok)
         atomicAdd(&status[r.x].bad_objects, 1u);

@@ -28,7 +28,9 @@ SEG_PAST_LENGTH = 4
 SEG_BAD_CHECKSUM = 8
 SEG_TABLE_FULL = 16
 SEG_CYCLE = 32
-LOG_ENTRY_TYPE_OBJ = 2
+LOG_ENTRY_TYPE_OBJ = 2          # src/LogEntryTypes.h:35
+LOG_ENTRY_TYPE_OBJTOMB = 3      # src/LogEntryTypes.h:38
+LOG_ENTRY_TYPE_SAFEVERSION = 5  # src/LogEntryTypes.h:44
 
 REPLAY_SEED = 0x5245504C   # "REPL": value bytes of segment i use seed REPLAY_SEED + i
 OBJECT_OVERHEAD = 24 + 1 + 2 + 8   # Object::Header + KeyCount + CumulativeKeyLength + key
@@ -82,7 +84,8 @@ class RecoveryVerify:
     """Device tables for walking and verifying batches of segments on one GPU.
 
     verify(d_segments, certs) returns the per-segment status tensor
-    (int32 [nseg, 4]: flags, checksum, entries, bad_objects) after both
+    (int32 [nseg, 4]: flags, checksum, entries, bad_objects -- failed object,
+    tombstone and safe-version checks) after both
     kernels ran on the current stream."""
 
     def __init__(self, ctx, nseg, capacity, stride=None, entries_cap=None, min_entry=None):

@@ -73,7 +73,7 @@ def build_batch(oracle, seed=1234):
             s[:] = 0
             certs[i] = (0, 0x48674BC7)   # src/SegmentTest.cc:369
         elif kind == "nonobj":
-            s[0] = (s[0] & 0xC0) | 3     # first entry becomes an OBJTOMB
+            s[0] = (s[0] & 0xC0) | 4     # first entry becomes a LOGDIGEST (replay checks no CRC)
         elif kind == "tiny_obj":
             # an OBJ entry shorter than Object::Header (length 5): counts as bad
             s[:8] = np.array([0x02, 5, 1, 2, 3, 4, 5, 0], np.uint8)
@@ -103,3 +103,85 @@ def oracle_walk(oracle, buf, certs, nseg, cap=CAPACITY):
     bad_total, crc, bad = oracle.verify_objects(buf, cap, table, nseg, seg_ok=ok)
     status[:, 3] = bad
     return status, table, crc
+
+
+def _log_entry(etype, payload):
+    """EntryHeader + little-endian length + payload (src/Segment.h:114-195)."""
+    n = len(payload)
+    lb = 1 if n < 1 << 8 else 2 if n < 1 << 16 else 3 if n < 1 << 24 else 4
+    return bytes([etype | ((lb - 1) << 6)]) + n.to_bytes(lb, "little") + payload
+
+
+def replay_mix_entries(oracle, golden, seed):
+    """Entries of every type ObjectManager::replaySegment checksums, valid and
+    damaged: [(entry bytes, expect_ok)] with expect_ok None for types it does
+    not checksum.  Anchored on the reference goldens: the object of
+    src/ObjectTest.cc:171 and the tombstone of src/ObjectTest.cc:913."""
+    rng = np.random.default_rng(seed)
+    u32 = lambda v: int(v).to_bytes(4, "little")
+    g = golden["object_checksums"][0]
+    obj = u32(g["checksum"]) + bytes.fromhex(g["bytes"])
+    t = golden["tombstone_checksums"][0]
+    tb = bytes.fromhex(t["bytes"])
+    tomb = tb[:28] + u32(t["checksum"]) + tb[28:]
+
+    def flip(b, i):
+        b = bytearray(b)
+        b[i] ^= 0x40
+        return bytes(b)
+
+    def tomb_of(key):
+        hdr = rng.integers(0, 256, 28, dtype=np.uint8).tobytes()
+        return hdr + u32(oracle.crc32c(np.frombuffer(hdr + key, np.uint8))) + key
+
+    def safe_of(ver, extra=b""):
+        h = int(ver).to_bytes(8, "little")
+        return h + u32(oracle.crc32c(np.frombuffer(h, np.uint8))) + extra
+
+    key = rng.integers(0, 256, int(rng.integers(300, 700)), dtype=np.uint8).tobytes()
+    e = [
+        (_log_entry(segments.LOG_ENTRY_TYPE_OBJ, obj), True),
+        (_log_entry(segments.LOG_ENTRY_TYPE_OBJTOMB, tomb), True),
+        (_log_entry(segments.LOG_ENTRY_TYPE_OBJTOMB, flip(tomb, 33)), False),   # key byte
+        (_log_entry(segments.LOG_ENTRY_TYPE_OBJTOMB, flip(tomb, 29)), False),   # stored checksum
+        (_log_entry(segments.LOG_ENTRY_TYPE_OBJTOMB, flip(tomb, 3)), False),    # header byte
+        (_log_entry(segments.LOG_ENTRY_TYPE_OBJTOMB, tomb_of(key)), True),      # 2 length bytes
+        (_log_entry(segments.LOG_ENTRY_TYPE_OBJTOMB, tomb_of(b"")), True),      # empty key
+        (_log_entry(segments.LOG_ENTRY_TYPE_OBJTOMB, tomb[:20]), False),        # shorter than its header
+        (_log_entry(segments.LOG_ENTRY_TYPE_SAFEVERSION, safe_of(rng.integers(1 << 62))), True),
+        (_log_entry(segments.LOG_ENTRY_TYPE_SAFEVERSION, flip(safe_of(7), 2)), False),
+        (_log_entry(segments.LOG_ENTRY_TYPE_SAFEVERSION, safe_of(9)[:8]), False),
+        (_log_entry(segments.LOG_ENTRY_TYPE_SAFEVERSION, safe_of(11, b"\x01\x02\x03\x04")), True),
+        (_log_entry(4, rng.integers(0, 256, 40, dtype=np.uint8).tobytes()), None),   # LOGDIGEST
+        (_log_entry(segments.LOG_ENTRY_TYPE_OBJ, flip(obj, len(obj) - 1)), False),
+    ]
+    order = rng.permutation(len(e))
+    return [e[i] for i in order]
+
+
+def build_replay_mix(oracle, golden, nseg=8, seed=77, cap=CAPACITY):
+    """nseg segments filled with replay_mix_entries groups; certificates from
+    the oracle's metadata checksum.  Returns (buf, certs, expected bad per
+    segment, expected checked records per segment)."""
+    buf = np.zeros(nseg * cap, np.uint8)
+    certs = np.zeros((nseg, 2), np.uint32)
+    bad = np.zeros(nseg, np.uint32)
+    checked = np.zeros(nseg, np.uint32)
+    for i in range(nseg):
+        s = _seg(buf, i, cap)
+        pos, k = 0, 0
+        while True:
+            group = replay_mix_entries(oracle, golden, seed * 1000 + i * 100 + k)
+            size = sum(len(b) for b, _ in group)
+            if pos + size > cap - 64 or k == 3 + i:
+                break
+            for b, ok in group:
+                s[pos:pos + len(b)] = np.frombuffer(b, np.uint8)
+                pos += len(b)
+                if ok is not None:
+                    checked[i] += 1
+                    bad[i] += 0 if ok else 1
+            k += 1
+        _, ck, _, _ = oracle.check_metadata(s, pos, 0)
+        certs[i] = (pos, ck)
+    return buf, certs, bad, checked

@@ -99,3 +99,26 @@ def test_walk_table_full_flag(ramcrc, oracle_mod):
     assert n == counts.sum()
     assert (status[:, 0] & segments.SEG_TABLE_FULL).any()
     assert ((status[:, 0] & segments.SEG_OK) != 0).all()
+
+
+@pytest.mark.gpu
+def test_walk_verify_replay_mix(ramcrc, oracle_mod, golden):
+    """Tombstones (src/ObjectManager.cc:752-758) and safe versions (:873-880)
+    beside objects, valid and damaged: per-segment failure counts, the record
+    table and every computed CRC equal the oracle's."""
+    buf, certs, bad, _ = segment_cases.build_replay_mix(oracle_mod, golden)
+    nseg, cap = certs.shape[0], segment_cases.CAPACITY
+    exp_status, exp_table, exp_crc = segment_cases.oracle_walk(oracle_mod, buf, certs, nseg)
+    assert np.array_equal(exp_status[:, 3], bad)
+    status, n, table, crc = _run(ramcrc, buf, certs, nseg, cap, nseg * 4096)
+    assert np.array_equal(status, exp_status)
+    assert n == exp_table.shape[0]
+    t_dev, c_dev = _sorted(table, crc)
+    t_exp, c_exp = _sorted(exp_table, exp_crc)
+    assert np.array_equal(t_dev, t_exp)
+    typ = t_exp[:, 3] & 0x13F
+    hdr = np.select([typ == segments.LOG_ENTRY_TYPE_OBJ, typ == segments.LOG_ENTRY_TYPE_OBJTOMB,
+                     typ == segments.LOG_ENTRY_TYPE_SAFEVERSION], [24, 32, 12], 1 << 32)
+    live = t_exp[:, 2] >= hdr
+    assert (typ[live] == segments.LOG_ENTRY_TYPE_OBJTOMB).sum() > 10
+    assert np.array_equal(c_dev[live], c_exp[live])

@@ -107,3 +107,30 @@ def test_oracle_damage_cases(oracle_mod):
             assert f == segments.SEG_CYCLE, (kind, f)
         elif kind == "tiny_obj":
             assert f == segments.SEG_OK and bad == 1, (kind, f, bad)
+
+
+def test_oracle_tombstone_golden(oracle_mod, golden):
+    """src/ObjectTest.cc:913: the tombstone's checksum is 0x5D60E8EF; replay
+    (src/ObjectManager.cc:752-758) checks it over header [0, 28) + key."""
+    t = golden["tombstone_checksums"][0]
+    tb = bytes.fromhex(t["bytes"])
+    tomb = tb[:28] + int(t["checksum"]).to_bytes(4, "little") + tb[28:]
+    seg = np.zeros(256, np.uint8)
+    e = segment_cases._log_entry(segments.LOG_ENTRY_TYPE_OBJTOMB, tomb)
+    seg[:len(e)] = np.frombuffer(e, np.uint8)
+    _, ck, n, table = oracle_mod.check_metadata(seg, len(e), 0)
+    bad, crc, _ = oracle_mod.verify_objects(seg, 256, table)
+    assert n == 1 and bad == 0 and crc[0] == t["checksum"]
+    seg[len(e) - 1] ^= 1   # last key byte
+    bad, _, _ = oracle_mod.verify_objects(seg, 256, table)
+    assert bad == 1
+
+
+def test_oracle_replay_mix(oracle_mod, golden):
+    """Objects, tombstones and safe versions, valid and damaged, plus an
+    unchecked type: the oracle's replay checks fail exactly the damaged ones."""
+    buf, certs, bad, checked = segment_cases.build_replay_mix(oracle_mod, golden)
+    status, table, crc = segment_cases.oracle_walk(oracle_mod, buf, certs, certs.shape[0])
+    assert (status[:, 0] == segments.SEG_OK).all()
+    assert np.array_equal(status[:, 3], bad)
+    assert bad.sum() > 0 and (checked > bad).all()
