@@ -149,8 +149,9 @@ typedef struct ramcrc_seg_status {
     uint32_t flags;        /* RAMCRC_SEG_* */
     uint32_t checksum;     /* metadata checksum the walk computed (over the entries walked + length) */
     uint32_t entries;      /* entries walked */
-    uint32_t bad_objects;  /* replay records whose checksum check failed: objects, tombstones
-                              and safe versions (see ramcrc_verify_objects_device) */
+    uint32_t bad_objects;  /* replay records whose checksum check failed: objects, tombstones,
+                              safe versions and transaction records (see
+                              ramcrc_verify_objects_device) */
 } ramcrc_seg_status;
 
 #define RAMCRC_SEG_OK 1u              /* Segment::checkMetadataIntegrity returned true */
@@ -163,6 +164,10 @@ typedef struct ramcrc_seg_status {
 #define RAMCRC_LOG_ENTRY_TYPE_OBJ 2u          /* LOG_ENTRY_TYPE_OBJ, src/LogEntryTypes.h:35 */
 #define RAMCRC_LOG_ENTRY_TYPE_OBJTOMB 3u      /* LOG_ENTRY_TYPE_OBJTOMB, src/LogEntryTypes.h:38 */
 #define RAMCRC_LOG_ENTRY_TYPE_SAFEVERSION 5u  /* LOG_ENTRY_TYPE_SAFEVERSION, src/LogEntryTypes.h:44 */
+#define RAMCRC_LOG_ENTRY_TYPE_PREP 8u         /* LOG_ENTRY_TYPE_PREP, src/LogEntryTypes.h:53 */
+#define RAMCRC_LOG_ENTRY_TYPE_PREPTOMB 9u     /* LOG_ENTRY_TYPE_PREPTOMB, src/LogEntryTypes.h:56 */
+#define RAMCRC_LOG_ENTRY_TYPE_TXDECISION 10u  /* LOG_ENTRY_TYPE_TXDECISION, src/LogEntryTypes.h:59 */
+#define RAMCRC_LOG_ENTRY_TYPE_TXPLIST 11u     /* LOG_ENTRY_TYPE_TXPLIST, src/LogEntryTypes.h:62 */
 
 /* Segment::checkMetadataIntegrity (src/Segment.cc:758-800) for n_seg segments
  * at d_base + i*seg_stride, each of seg_capacity bytes (a multiple of 16; the
@@ -191,12 +196,29 @@ int ramcrc_segment_walk_device(ramcrc_ctx* ctx, const void* d_base, uint64_t seg
  *                               the key [32, length) vs. the checksum at [28, 32);
  *   LOG_ENTRY_TYPE_SAFEVERSION  ObjectSafeVersion::checkIntegrity
  *                               (src/ObjectManager.cc:873-880): bytes [0, 8) vs.
- *                               the checksum at [8, 12).
+ *                               the checksum at [8, 12);
+ *   LOG_ENTRY_TYPE_PREP         PreparedOp::checkIntegrity (src/ObjectManager.cc:956,
+ *                               src/PreparedOp.cc:177-190): header bytes [0, 28)
+ *                               and the object from its byte 4, [36, length), vs.
+ *                               the checksum at [28, 32);
+ *   LOG_ENTRY_TYPE_PREPTOMB     PreparedOpTombstone::checkIntegrity (:1013,
+ *                               src/PreparedOp.cc:271-282): bytes [0, 40) vs. [40, 44);
+ *   LOG_ENTRY_TYPE_TXDECISION   TxDecisionRecord::checkIntegrity (:1060,
+ *                               src/TxDecisionRecord.cc:209-223): bytes [0, 44) and
+ *                               24 * participantCount (uint32, at [36, 40)) bytes
+ *                               from 48, clipped to the entry as Buffer::Iterator
+ *                               does, vs. the checksum at [44, 48);
+ *   LOG_ENTRY_TYPE_TXPLIST      ParticipantList::checkIntegrity (:1084,
+ *                               src/ParticipantList.cc:96-110): bytes [0, 20) and
+ *                               24 * participantCount (uint32, at [16, 20)) bytes
+ *                               from 24 vs. the checksum at [20, 24); a list
+ *                               longer than the entry fails (the reference's
+ *                               getRange returns NULL there).
  * The computed CRC goes to d_obj_crc[i] (other records: not written), and
  * d_status[segment].bad_objects += 1 per failed check (records shorter than
- * their type's header, 24 / 32 / 12 bytes, or flagged OVERLONG fail).  Objects
- * of >= 64 KiB are scanned by all CUs, smaller ones by the small-entry
- * kernels; tombstones and safe versions by one thread each.  Stream-ordered
+ * their type's header, 24 / 32 / 12 / 56 / 44 / 48 / 24 bytes, or flagged
+ * OVERLONG fail).  Objects of >= 64 KiB are scanned by all CUs, smaller ones
+ * by the small-entry kernels; the other types by one thread each.  Stream-ordered
  * after the walk that produced the table. */
 int ramcrc_verify_objects_device(ramcrc_ctx* ctx, const void* d_base, uint64_t seg_stride,
                                  const ramcrc_seg_entry* d_entries, uint64_t entries_cap,

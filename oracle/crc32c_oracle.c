@@ -421,9 +421,27 @@ uint32_t oracle_check_metadata(const uint8_t* seg, uint64_t capacity, uint32_t c
  *                    header.checksum at [28, 32) (src/ObjectManager.cc:752-758);
  *   SAFEVERSION (5)  ObjectSafeVersion::computeChecksum (src/Object.cc:1135-1143):
  *                    bytes [0, 8) against header.checksum at [8, 12)
- *                    (src/ObjectManager.cc:873-880).
+ *                    (src/ObjectManager.cc:873-880);
+ *   PREP (8)         PreparedOp::computeChecksum (src/PreparedOp.cc:177-190):
+ *                    its header (src/PreparedOp.h:63-100, 32 bytes) up to the
+ *                    checksum, [0, 28), then Object::applyChecksum of the
+ *                    object at 32 (src/Object.cc:748-765): [36, len); against
+ *                    [28, 32) (src/ObjectManager.cc:956);
+ *   PREPTOMB (9)     PreparedOpTombstone::computeChecksum (src/PreparedOp.cc:271-282):
+ *                    [0, 40) of the 44-byte header against [40, 44) (:1013);
+ *   TXDECISION (10)  TxDecisionRecord::computeChecksum (src/TxDecisionRecord.cc:209-223):
+ *                    [0, 44) of the 48-byte header, then
+ *                    sizeof32(TxParticipant) * participantCount (uint32 product;
+ *                    count at [36, 40)) bytes from 48 through a Buffer::Iterator,
+ *                    which clips to the entry (src/Buffer.cc:838-868); against
+ *                    [44, 48) (:1060);
+ *   TXPLIST (11)     ParticipantList::computeChecksum (src/ParticipantList.cc:96-110):
+ *                    [0, 20) of the 24-byte header, then 24 * count (count at
+ *                    [16, 20)) bytes from 24, against [20, 24) (:1084).  A list
+ *                    past the entry fails: getRange (src/Buffer.cc:530-549)
+ *                    returns NULL there and the reference would fault.
  * crc_out[i] receives the computed CRC of each readable record of these types
- * that holds at least its header (24, 32, 12 bytes).  Returns the number of
+ * that holds at least its header (24, 32, 12, 56, 44, 48, 24 bytes).  Returns the number of
  * failed checks; shorter or unreadable records count as failures (the
  * reference would read past the entry there).  Failures are added to
  * bad_per_seg[segment] when that is non-NULL. */
@@ -438,26 +456,44 @@ uint64_t oracle_verify_objects(const uint8_t* base, uint64_t stride, const uint3
     for (uint64_t i = 0; i < n; i++) {
         const uint32_t* r = table + 4 * i;
         const uint32_t type = r[3] & 0x3f;
-        if ((type != 2 && type != 3 && type != 5) || (seg_ok && !seg_ok[r[0]]))
+        static const uint32_t hdr_of[12] = {0, 0, 24, 32, 0, 12, 0, 0, 56, 44, 48, 24};
+        const uint32_t hdr = type < 12 ? hdr_of[type] : 0;
+        if (hdr == 0 || (seg_ok && !seg_ok[r[0]]))
             continue;
-        const uint32_t hdr = type == 2 ? 24u : type == 3 ? 32u : 12u;
         int ok = 0;
         if (r[2] >= hdr && !(r[3] & 0x100)) {
             const uint8_t* payload = base + (uint64_t)r[0] * stride + r[1] + 1 + ((r[3] >> 6) & 3) + 1;
+            const uint32_t len = r[2];
             uint32_t c, stored;
+            int fits = 1;
             if (type == 2) {
-                c = ~f(0xFFFFFFFFu, payload + 4, r[2] - 4);
+                c = ~f(0xFFFFFFFFu, payload + 4, len - 4);
                 stored = oracle_u32le(payload);
-            } else if (type == 3) {
-                c = ~f(f(0xFFFFFFFFu, payload, 28), payload + 32, r[2] - 32);
-                stored = oracle_u32le(payload + 28);
             } else {
-                c = ~f(0xFFFFFFFFu, payload, 8);
-                stored = oracle_u32le(payload + 8);
+                /* CRC of [0, at) then [from, from + tail); checksum at [at, at + 4) */
+                uint32_t at = hdr - 4, from = hdr, tail = 0;
+                if (type == 3) {
+                    tail = len - 32;
+                } else if (type == 8) {
+                    at = 28;
+                    from = 36;
+                    tail = len - 36;
+                } else if (type == 10) {
+                    tail = 24u * oracle_u32le(payload + 36);
+                    if (tail > len - 48)
+                        tail = len - 48;
+                } else if (type == 11) {
+                    tail = 24u * oracle_u32le(payload + 16);
+                    fits = tail <= len - 24;
+                }
+                c = ~f(f(0xFFFFFFFFu, payload, at), payload + from, fits ? tail : 0);
+                stored = oracle_u32le(payload + at);
             }
-            if (crc_out)
-                crc_out[i] = c;
-            ok = c == stored;
+            if (fits) {
+                if (crc_out)
+                    crc_out[i] = c;
+                ok = c == stored;
+            }
         }
         if (!ok) {
             bad++;

@@ -369,6 +369,10 @@ enum Mode { kSegAligned = 0, kSegUniform = 1, kTable = 2, kRecords = 3, kObjects
 constexpr uint32_t kObjHeaderBytes = 24;     // Object::Header, src/Object.h:137-182
 constexpr uint32_t kTombHeaderBytes = 32;    // ObjectTombstone::Header, src/Object.h:285-338
 constexpr uint32_t kSafeVersionBytes = 12;   // ObjectSafeVersion::Header, src/Object.h:402-427
+constexpr uint32_t kPrepHeaderBytes = 32;    // PreparedOp::Header, src/PreparedOp.h:63-100
+constexpr uint32_t kPrepTombBytes = 44;      // PreparedOpTombstone::Header, src/PreparedOp.h:142-185
+constexpr uint32_t kTxDecisionHeaderBytes = 48;  // TxDecisionRecord::Header, src/TxDecisionRecord.h:62-128
+constexpr uint32_t kTxPlistHeaderBytes = 24;     // ParticipantList::Header, src/ParticipantList.h:81-113
 constexpr uint32_t kRecOverlong = 0x100;   // record header bit: payload past the capacity
 
 template <int kMode>
@@ -2014,10 +2018,24 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
 //                src/Object.cc:1014-1057): CRC of header bytes [0, 28) and the
 //                key [32, len) vs. the checksum at [28, 32);
 //   SAFEVERSION  ObjectSafeVersion::checkIntegrity (src/ObjectManager.cc:873-880,
-//                src/Object.cc:1107-1143): CRC of [0, 8) vs. the checksum at [8, 12).
-// Tombstones and safe versions are rare and short (a key), so one thread runs
-// the byte-table CRC over each and writes it to d.out[i].  Records shorter
-// than their type's header, or unreadable, count as failures.
+//                src/Object.cc:1107-1143): CRC of [0, 8) vs. the checksum at [8, 12);
+//   PREP         PreparedOp::checkIntegrity (src/ObjectManager.cc:956,
+//                src/PreparedOp.cc:177-190): its 32-byte header up to the
+//                checksum, [0, 28), then Object::applyChecksum of the object at
+//                32, i.e. [36, len); checksum at [28, 32);
+//   PREPTOMB     PreparedOpTombstone::checkIntegrity (src/ObjectManager.cc:1013,
+//                src/PreparedOp.cc:271-282): [0, 40) vs. [40, 44);
+//   TXDECISION   TxDecisionRecord::checkIntegrity (src/ObjectManager.cc:1060,
+//                src/TxDecisionRecord.cc:209-223): [0, 44) and the uint32
+//                24 * participantCount (at [36, 40)) bytes from 48, clipped to
+//                the entry as Buffer::Iterator clips; checksum at [44, 48);
+//   TXPLIST      ParticipantList::checkIntegrity (src/ObjectManager.cc:1084,
+//                src/ParticipantList.cc:96-110): [0, 20) and 24 * count (at
+//                [16, 20)) bytes from 24; checksum at [20, 24).  A list longer
+//                than the entry fails: the reference's getRange returns NULL.
+// All but OBJ are rare, and short apart from a prepared op's object, so one
+// thread runs the byte-table CRC over each and writes it to d.out[i].
+// Records shorter than their type's header, or unreadable, count as failures.
 __device__ __forceinline__ uint32_t crc_bytes_g(const uint32_t* t1, uint32_t c, const gu8* p,
                                                 uint32_t n)
 {
@@ -2031,6 +2049,21 @@ __device__ __forceinline__ uint32_t le32_g(const gu8* p)
     return uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
 }
 
+// Header bytes a record of `type` must hold to be checked; 0 = not checked.
+__device__ __forceinline__ uint32_t replay_header_bytes(uint32_t type)
+{
+    switch (type) {
+    case RAMCRC_LOG_ENTRY_TYPE_OBJ: return kObjHeaderBytes;
+    case RAMCRC_LOG_ENTRY_TYPE_OBJTOMB: return kTombHeaderBytes;
+    case RAMCRC_LOG_ENTRY_TYPE_SAFEVERSION: return kSafeVersionBytes;
+    case RAMCRC_LOG_ENTRY_TYPE_PREP: return kPrepHeaderBytes + kObjHeaderBytes;
+    case RAMCRC_LOG_ENTRY_TYPE_PREPTOMB: return kPrepTombBytes;
+    case RAMCRC_LOG_ENTRY_TYPE_TXDECISION: return kTxDecisionHeaderBytes;
+    case RAMCRC_LOG_ENTRY_TYPE_TXPLIST: return kTxPlistHeaderBytes;
+    default: return 0;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_obj_compare(BatchDesc d, ramcrc_seg_status* status)
 {
     const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -2038,13 +2071,9 @@ __global__ __launch_bounds__(256) void k_obj_compare(BatchDesc d, ramcrc_seg_sta
         return;
     const u32x4 r = d.rec[i];
     const uint32_t type = r.w & 0x3f;
-    if ((type != RAMCRC_LOG_ENTRY_TYPE_OBJ && type != RAMCRC_LOG_ENTRY_TYPE_OBJTOMB &&
-         type != RAMCRC_LOG_ENTRY_TYPE_SAFEVERSION) ||
-        !(d.seg_status[r.x].x & RAMCRC_SEG_OK))
+    const uint32_t hdr = replay_header_bytes(type);
+    if (hdr == 0 || !(d.seg_status[r.x].x & RAMCRC_SEG_OK))
         return;
-    const uint32_t hdr = type == RAMCRC_LOG_ENTRY_TYPE_OBJ ? kObjHeaderBytes
-                         : type == RAMCRC_LOG_ENTRY_TYPE_OBJTOMB ? kTombHeaderBytes
-                                                                 : kSafeVersionBytes;
     bool ok = false;
     if (r.z >= hdr && !(r.w & kRecOverlong)) {
         const uint64_t payload = reinterpret_cast<uint64_t>(d.base) + uint64_t(r.x) * d.seg_bytes +
@@ -2053,14 +2082,31 @@ __global__ __launch_bounds__(256) void k_obj_compare(BatchDesc d, ramcrc_seg_sta
         if (type == RAMCRC_LOG_ENTRY_TYPE_OBJ) {
             ok = d.out[i] == le32_g(p);
         } else {
-            const uint32_t* t1 = &g_tab.pos[1 + kTinyRow0][0];   // X^1(b): the byte step
-            uint32_t c;
-            if (type == RAMCRC_LOG_ENTRY_TYPE_OBJTOMB)
-                c = ~crc_bytes_g(t1, crc_bytes_g(t1, 0xFFFFFFFFu, p, 28), p + 32, r.z - 32);
-            else
-                c = ~crc_bytes_g(t1, 0xFFFFFFFFu, p, 8);
-            d.out[i] = c;
-            ok = c == le32_g(p + hdr - 4);
+            // CRC of [0, at) then of [from, from + tail); stored checksum at [at, at + 4)
+            uint32_t at = hdr - 4, from = hdr, tail = 0;
+            bool fits = true;
+            switch (type) {
+            case RAMCRC_LOG_ENTRY_TYPE_OBJTOMB: tail = r.z - hdr; break;
+            case RAMCRC_LOG_ENTRY_TYPE_PREP:
+                at = kPrepHeaderBytes - 4;
+                from = kPrepHeaderBytes + 4;
+                tail = r.z - from;
+                break;
+            case RAMCRC_LOG_ENTRY_TYPE_TXDECISION:
+                tail = min(24u * le32_g(p + 36), r.z - hdr);
+                break;
+            case RAMCRC_LOG_ENTRY_TYPE_TXPLIST:
+                tail = 24u * le32_g(p + 16);
+                fits = tail <= r.z - hdr;
+                break;
+            default: break;
+            }
+            if (fits) {
+                const uint32_t* t1 = &g_tab.pos[1 + kTinyRow0][0];   // X^1(b): the byte step
+                const uint32_t c = ~crc_bytes_g(t1, crc_bytes_g(t1, 0xFFFFFFFFu, p, at), p + from, tail);
+                d.out[i] = c;
+                ok = c == le32_g(p + at);
+            }
         }
     }
     if (!ok)

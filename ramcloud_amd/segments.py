@@ -31,6 +31,18 @@ SEG_CYCLE = 32
 LOG_ENTRY_TYPE_OBJ = 2          # src/LogEntryTypes.h:35
 LOG_ENTRY_TYPE_OBJTOMB = 3      # src/LogEntryTypes.h:38
 LOG_ENTRY_TYPE_SAFEVERSION = 5  # src/LogEntryTypes.h:44
+LOG_ENTRY_TYPE_PREP = 8         # src/LogEntryTypes.h:53
+LOG_ENTRY_TYPE_PREPTOMB = 9     # src/LogEntryTypes.h:56
+LOG_ENTRY_TYPE_TXDECISION = 10  # src/LogEntryTypes.h:59
+LOG_ENTRY_TYPE_TXPLIST = 11     # src/LogEntryTypes.h:62
+# Bytes a replayed record of each checked type must hold (ObjectManager::replaySegment,
+# src/ObjectManager.cc:659-1100): Object::Header, ObjectTombstone::Header,
+# ObjectSafeVersion::Header, PreparedOp::Header + Object::Header,
+# PreparedOpTombstone::Header, TxDecisionRecord::Header, ParticipantList::Header.
+REPLAY_HEADER_BYTES = {LOG_ENTRY_TYPE_OBJ: 24, LOG_ENTRY_TYPE_OBJTOMB: 32,
+                       LOG_ENTRY_TYPE_SAFEVERSION: 12, LOG_ENTRY_TYPE_PREP: 56,
+                       LOG_ENTRY_TYPE_PREPTOMB: 44, LOG_ENTRY_TYPE_TXDECISION: 48,
+                       LOG_ENTRY_TYPE_TXPLIST: 24}
 
 REPLAY_SEED = 0x5245504C   # "REPL": value bytes of segment i use seed REPLAY_SEED + i
 OBJECT_OVERHEAD = 24 + 1 + 2 + 8   # Object::Header + KeyCount + CumulativeKeyLength + key

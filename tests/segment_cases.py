@@ -138,6 +138,38 @@ def replay_mix_entries(oracle, golden, seed):
         h = int(ver).to_bytes(8, "little")
         return h + u32(oracle.crc32c(np.frombuffer(h, np.uint8))) + extra
 
+    def rand(n):
+        return rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+
+    def crc(b):
+        return u32(oracle.crc32c(np.frombuffer(b, np.uint8)))
+
+    # PreparedOp (src/PreparedOp.h:63-100, src/PreparedOp.cc:177-190): 32-byte
+    # header, checksum at [28, 32) over [0, 28) and the object from its byte 4
+    def prep_of(o):
+        h = rand(28)
+        return h + crc(h + o[4:]) + o
+
+    # PreparedOpTombstone (src/PreparedOp.h:142-185, src/PreparedOp.cc:271-282)
+    def preptomb_of():
+        h = rand(40)
+        return h + crc(h)
+
+    # TxDecisionRecord (src/TxDecisionRecord.h:62-128, .cc:209-223): participants
+    # through Buffer::Iterator, uint32 24 * count clipped to the entry
+    def txdec_of(count, present):
+        h = rand(36) + u32(count) + rand(4)
+        parts = rand(24 * present)
+        tail = min((24 * count) & 0xFFFFFFFF, len(parts))
+        return h + crc(h + parts[:tail]) + parts
+
+    # ParticipantList (src/ParticipantList.h:81-113, .cc:96-110)
+    def txplist_of(count):
+        h = rand(16) + u32(count)
+        parts = rand(24 * count)
+        return h + crc(h + parts) + parts
+
+    big = u32(0) + bytes.fromhex(g["bytes"])[:20] + rand(int(rng.integers(1500, 2500)))
     key = rng.integers(0, 256, int(rng.integers(300, 700)), dtype=np.uint8).tobytes()
     e = [
         (_log_entry(segments.LOG_ENTRY_TYPE_OBJ, obj), True),
@@ -154,9 +186,48 @@ def replay_mix_entries(oracle, golden, seed):
         (_log_entry(segments.LOG_ENTRY_TYPE_SAFEVERSION, safe_of(11, b"\x01\x02\x03\x04")), True),
         (_log_entry(4, rng.integers(0, 256, 40, dtype=np.uint8).tobytes()), None),   # LOGDIGEST
         (_log_entry(segments.LOG_ENTRY_TYPE_OBJ, flip(obj, len(obj) - 1)), False),
+        (_log_entry(segments.LOG_ENTRY_TYPE_PREP, prep_of(obj)), True),            # golden object inside
+        (_log_entry(segments.LOG_ENTRY_TYPE_PREP, prep_of(big)), True),            # 2 length bytes
+        (_log_entry(segments.LOG_ENTRY_TYPE_PREP, flip(prep_of(obj), 33)), True),  # object's own checksum: not covered
+        (_log_entry(segments.LOG_ENTRY_TYPE_PREP, flip(prep_of(obj), 40)), False),  # object header byte
+        (_log_entry(segments.LOG_ENTRY_TYPE_PREP, flip(prep_of(big), 32 + 24 + 1000)), False),
+        (_log_entry(segments.LOG_ENTRY_TYPE_PREP, flip(prep_of(obj), 30)), False),  # stored checksum
+        (_log_entry(segments.LOG_ENTRY_TYPE_PREP, prep_of(obj)[:50]), False),      # shorter than its headers
+        (_log_entry(segments.LOG_ENTRY_TYPE_PREPTOMB, preptomb_of()), True),
+        (_log_entry(segments.LOG_ENTRY_TYPE_PREPTOMB, flip(preptomb_of(), 39)), False),
+        (_log_entry(segments.LOG_ENTRY_TYPE_PREPTOMB, preptomb_of()[:43]), False),
+        (_log_entry(segments.LOG_ENTRY_TYPE_TXDECISION, txdec_of(3, 3)), True),
+        (_log_entry(segments.LOG_ENTRY_TYPE_TXDECISION, txdec_of(0, 0)), True),
+        (_log_entry(segments.LOG_ENTRY_TYPE_TXDECISION, txdec_of(5, 2)), True),     # count past the entry: clipped
+        (_log_entry(segments.LOG_ENTRY_TYPE_TXDECISION, txdec_of(0xAAAAAAAB, 1)), True),  # 24 * count wraps to 8
+        (_log_entry(segments.LOG_ENTRY_TYPE_TXDECISION, txdec_of(2, 2) + rand(5)), True),  # bytes past the list
+        (_log_entry(segments.LOG_ENTRY_TYPE_TXDECISION, flip(txdec_of(3, 3), 100)), False),
+        (_log_entry(segments.LOG_ENTRY_TYPE_TXDECISION, flip(txdec_of(3, 3), 37)), False),  # count byte
+        (_log_entry(segments.LOG_ENTRY_TYPE_TXDECISION, txdec_of(0, 0)[:47]), False),
+        (_log_entry(segments.LOG_ENTRY_TYPE_TXPLIST, txplist_of(4)), True),
+        (_log_entry(segments.LOG_ENTRY_TYPE_TXPLIST, txplist_of(0)), True),
+        (_log_entry(segments.LOG_ENTRY_TYPE_TXPLIST, flip(txplist_of(4), 60)), False),
+        (_log_entry(segments.LOG_ENTRY_TYPE_TXPLIST, txplist_of(4)[:-1]), False),   # list past the entry
+        (_log_entry(segments.LOG_ENTRY_TYPE_TXPLIST, txplist_of(1)[:23]), False),
+        (_log_entry(7, rand(60)), None),                                            # RPCRESULT: not checked
     ]
     order = rng.permutation(len(e))
     return [e[i] for i in order]
+
+
+def replay_crc_mask(buf, cap, table):
+    """Records the replay checks leave a computed CRC for: those of a checked
+    type holding their header, not OVERLONG, and (ParticipantList) whose list
+    fits in the entry."""
+    typ = table[:, 3] & 0x3F
+    hdr = np.array([segments.REPLAY_HEADER_BYTES.get(int(t), 1 << 32) for t in typ], np.int64)
+    m = (table[:, 2] >= hdr) & ((table[:, 3] & 0x100) == 0)
+    for i in np.nonzero(m & (typ == segments.LOG_ENTRY_TYPE_TXPLIST))[0]:
+        seg, off, ln, h = (int(v) for v in table[i])
+        p = seg * cap + off + 1 + ((h >> 6) & 3) + 1
+        count = int.from_bytes(bytes(buf[p + 16:p + 20]), "little")
+        m[i] = (24 * count) & 0xFFFFFFFF <= ln - 24
+    return m
 
 
 def build_replay_mix(oracle, golden, nseg=8, seed=77, cap=CAPACITY):

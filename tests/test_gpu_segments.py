@@ -103,8 +103,9 @@ def test_walk_table_full_flag(ramcrc, oracle_mod):
 
 @pytest.mark.gpu
 def test_walk_verify_replay_mix(ramcrc, oracle_mod, golden):
-    """Tombstones (src/ObjectManager.cc:752-758) and safe versions (:873-880)
-    beside objects, valid and damaged: per-segment failure counts, the record
+    """Tombstones (src/ObjectManager.cc:752-758), safe versions (:873-880) and
+    the transaction records (prepared ops and their tombstones, decision
+    records, participant lists: :956-1084) beside objects, valid and damaged: per-segment failure counts, the record
     table and every computed CRC equal the oracle's."""
     buf, certs, bad, _ = segment_cases.build_replay_mix(oracle_mod, golden)
     nseg, cap = certs.shape[0], segment_cases.CAPACITY
@@ -116,9 +117,9 @@ def test_walk_verify_replay_mix(ramcrc, oracle_mod, golden):
     t_dev, c_dev = _sorted(table, crc)
     t_exp, c_exp = _sorted(exp_table, exp_crc)
     assert np.array_equal(t_dev, t_exp)
-    typ = t_exp[:, 3] & 0x13F
-    hdr = np.select([typ == segments.LOG_ENTRY_TYPE_OBJ, typ == segments.LOG_ENTRY_TYPE_OBJTOMB,
-                     typ == segments.LOG_ENTRY_TYPE_SAFEVERSION], [24, 32, 12], 1 << 32)
-    live = t_exp[:, 2] >= hdr
-    assert (typ[live] == segments.LOG_ENTRY_TYPE_OBJTOMB).sum() > 10
+    typ = t_exp[:, 3] & 0x3F
+    live = segment_cases.replay_crc_mask(buf, cap, t_exp)
+    for t in (segments.LOG_ENTRY_TYPE_OBJTOMB, segments.LOG_ENTRY_TYPE_PREP,
+              segments.LOG_ENTRY_TYPE_TXDECISION, segments.LOG_ENTRY_TYPE_TXPLIST):
+        assert (typ[live] == t).sum() > 10
     assert np.array_equal(c_dev[live], c_exp[live])
