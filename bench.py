@@ -207,25 +207,106 @@ def run_replay(args, ctx):
                                                 threads=threads)
     d.copy_(torch.from_numpy(host))
     dc = torch.from_numpy(np.ascontiguousarray(certs).view(np.int32)).cuda()
-    rv = segments.RecoveryVerify(ctx, nseg, seg_bytes, entries_cap=int(counts.sum()) + nseg)
-    for _ in range(args.warmup):
-        rv.verify(d, dc)
+    cap = int(counts.sum()) + nseg
+    if args.walk_cus:
+        elapsed, scan_ms, launches, sts = _replay_pipelined(args, ctx, d, dc, nseg, seg_bytes, cap)
+    else:
+        rv = segments.RecoveryVerify(ctx, nseg, seg_bytes, entries_cap=cap)
+        for _ in range(args.warmup):
+            rv.verify(d, dc)
+        torch.cuda.synchronize()
+        ctx.set_timing(True)
+        ctx.scan_time()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            st = rv.verify(d, dc)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        scan_ms, launches = ctx.scan_time()
+        ctx.set_timing(False)
+        sts = [st]
+    ok = True
+    for st in sts:
+        status = st.cpu().numpy().view(np.uint32)
+        ok = ok and bool((status[:, 0] == segments.SEG_OK).all() and (status[:, 3] == 0).all()
+                         and np.array_equal(status[:, 2], counts)
+                         and np.array_equal(status[:, 1], certs[:, 1]))
+    return dict(seg_bytes=seg_bytes, nseg=nseg, counts=counts, certs=certs, host=host,
+                elapsed=elapsed, scan_ms=scan_ms, launches=launches, ok=ok)
+
+
+def _walk_cu_list(ncu, walk_cus):
+    """CUs for the walk stream: runs of 8 consecutive CU ids spread evenly
+    over the device, so every XCD gets an equal share whether CU ids map to
+    XCDs round-robin (id % 8) or in contiguous blocks (id // 32)."""
+    runs = walk_cus // 8
+    stride = ncu // 8 // runs
+    return [r * stride * 8 + j for r in range(runs) for j in range(8)]
+
+
+def _replay_pipelined(args, ctx, d, dc, nseg, seg_bytes, cap):
+    """Replay of a stream of segment batches (a recovery master replaying
+    batch after batch, src/ObjectManager.cc:580-1100) with the walk of batch k
+    on walk_cus CUs overlapped with the object scan of batch k-1 on the
+    others (ramcrc_stream_create_cu_mask).  Two batches alternate: the second
+    is a copy of the first at another HBM address.  Every timed step walks and
+    verifies exactly one whole batch: the first walk and the last scan are
+    inside the timed region."""
+    from ramcloud_amd import ramcrc, segments
+    dev = torch.cuda.current_device()
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    walk = _walk_cu_list(ncu, args.walk_cus)
+    rest = [c for c in range(ncu) if c not in set(walk)]
+    s_walk = ramcrc.CuMaskStream(dev, walk)
+    s_scan = ramcrc.CuMaskStream(dev, rest)
+    t_walk = torch.cuda.ExternalStream(s_walk.handle)
+    t_scan = torch.cuda.ExternalStream(s_scan.handle)
+    ctx_walk = ramcrc.Context(dev)
+    ctx.set_cus(len(rest))
+    bufs = [d, d.clone()]
+    rvs = [segments.RecoveryVerify(ctx, nseg, seg_bytes, entries_cap=cap) for _ in range(2)]
+    ev_walk = [torch.cuda.Event() for _ in range(2)]
+    ev_scan = [torch.cuda.Event() for _ in range(2)]
+    torch.cuda.synchronize()
+
+    def do_walk(k):
+        b = k % 2
+        if k >= 2:
+            t_walk.wait_event(ev_scan[b])   # batch k-2's scan has read table b
+        rv = rvs[b]
+        ctx_walk.segment_walk(bufs[b], rv.stride, rv.capacity, nseg, dc, rv.status, rv.entries,
+                              rv.n_entries, stream=s_walk)
+        ev_walk[b].record(t_walk)
+
+    def do_scan(k):
+        b = k % 2
+        t_scan.wait_event(ev_walk[b])
+        rvs[b].verify_objects(bufs[b], stream=s_scan)
+        ev_scan[b].record(t_scan)
+
+    def run(steps):
+        for k in range(steps):
+            do_walk(k)
+            if k:
+                do_scan(k - 1)
+        do_scan(steps - 1)
+
+    run(max(args.warmup, 2))
     torch.cuda.synchronize()
     ctx.set_timing(True)
     ctx.scan_time()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        st = rv.verify(d, dc)
+    run(args.steps)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     scan_ms, launches = ctx.scan_time()
     ctx.set_timing(False)
-    status = st.cpu().numpy().view(np.uint32)
-    ok = bool((status[:, 0] == segments.SEG_OK).all() and (status[:, 3] == 0).all()
-              and np.array_equal(status[:, 2], counts)
-              and np.array_equal(status[:, 1], certs[:, 1]))
-    return dict(seg_bytes=seg_bytes, nseg=nseg, counts=counts, certs=certs, host=host,
-                elapsed=elapsed, scan_ms=scan_ms, launches=launches, ok=ok)
+    sts = [rv.status.clone() for rv in rvs]
+    ctx.set_cus(0)
+    ctx_walk.close()
+    s_walk.destroy()
+    s_scan.destroy()
+    return elapsed, scan_ms, launches, sts
 
 
 def run_append(args, ctx):
@@ -351,6 +432,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=128, help="segments timed on the CPU")
     ap.add_argument("--replay-cpu-sample", type=int, default=16,
                     help="replay config: segments verified by the CPU baseline")
+    ap.add_argument("--walk-cus", type=int, default=0,
+                    help="replay config: pipeline batches, walking on this many CUs "
+                         "(a multiple of 8) beside the object scan on the rest; 0 = serial")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -471,6 +555,8 @@ def main():
             "data": "synthetic (RecoverSegmentBenchmark-shaped objects, splitmix64 values)",
             "config": {"workload": f"{r['nseg']} x {args.seg_mib} MiB segments of "
                                    f"{args.value_len} B-value objects",
+                       "pipeline": (f"walk on {args.walk_cus} CUs beside the scan of the previous batch"
+                                    if args.walk_cus else "none"),
                        "objects": int(r["counts"].sum()), "object_bytes_checksummed": obj_bytes},
             "roofline": {"bound": "hbm", "kernel": "k_entries (object verify)",
                          "achieved": round(achieved, 1) if achieved else None,

@@ -267,6 +267,22 @@ int ramcrc_assemble_objects_host(ramcrc_ctx* ctx, void* const* objs, const uint6
 int ramcrc_ctx_set_timing(ramcrc_ctx* ctx, int enable);
 int ramcrc_ctx_scan_time(ramcrc_ctx* ctx, double* total_ms, uint64_t* launches);
 
+/* Replay pipelining (a recovery master replaying a stream of segment batches,
+ * src/ObjectManager.cc:580-1100): the segment walk is one latency-bound wave
+ * per segment, the object scan a bandwidth-bound persistent grid whose
+ * workgroups take most of a CU's LDS, so the two cannot share CUs.
+ * ramcrc_stream_create_cu_mask creates a stream whose kernels run only on
+ * the CUs set in cu_mask (hipExtStreamCreateWithCUMask; bit i of word i/32 =
+ * CU i, mask_words <= 8); ramcrc_ctx_set_cus(ctx, n) sizes the context's
+ * persistent grids (k_chunks, k_entries*) for n CUs (0 = all of them), to
+ * match the mask of the stream the context launches on.  Walking batch k on
+ * one masked stream while batch k-1 is scanned on the complementary one
+ * overlaps the two. */
+int ramcrc_stream_create_cu_mask(int device, const uint32_t* cu_mask, uint32_t mask_words,
+                                 void** out_stream);
+int ramcrc_stream_destroy(void* stream);
+int ramcrc_ctx_set_cus(ramcrc_ctx* ctx, int ncu);
+
 /* Nonzero if a planned launch found more chunks than the context's scratch
  * holds (its outputs were not written); raise ramcrc_ctx_reserve.  Synchronous. */
 int ramcrc_ctx_status(ramcrc_ctx* ctx, uint32_t* status);

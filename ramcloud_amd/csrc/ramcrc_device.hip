@@ -1558,7 +1558,8 @@ struct DeviceGuard {
 
 struct ramcrc_ctx {
     int device = 0;
-    int ncu = 256;
+    int ncu = 256;       // CUs the persistent grids are sized for (ramcrc_ctx_set_cus)
+    int ncu_all = 256;   // CUs of the device
     std::mutex mu;
     uint32_t* partials = nullptr;
     uint64_t partials_cap = 0;
@@ -2191,6 +2192,7 @@ int ramcrc_ctx_create(int device, ramcrc_ctx** out)
         return RAMCRC_ENOMEM;
     c->device = device;
     c->ncu = prop.multiProcessorCount;
+    c->ncu_all = c->ncu;
     if (hipMalloc(reinterpret_cast<void**>(&c->status), 16) != hipSuccess) {
         delete c;
         return RAMCRC_ENOMEM;
@@ -2251,6 +2253,39 @@ int ramcrc_ctx_set_timing(ramcrc_ctx* c, int enable)
         return RAMCRC_EINVAL;
     std::lock_guard<std::mutex> lk(c->mu);
     c->timing = enable != 0;
+    return RAMCRC_OK;
+}
+
+int ramcrc_stream_create_cu_mask(int device, const uint32_t* cu_mask, uint32_t mask_words,
+                                 void** out_stream)
+{
+    if (!cu_mask || !out_stream || mask_words == 0 || mask_words > 8)
+        return RAMCRC_EINVAL;
+    DeviceGuard g(device);
+    if (!g.ok)
+        return RAMCRC_ENODEV;
+    hipStream_t st = nullptr;
+    HIPCHK(hipExtStreamCreateWithCUMask(&st, mask_words, cu_mask));
+    *out_stream = st;
+    return RAMCRC_OK;
+}
+
+int ramcrc_stream_destroy(void* stream)
+{
+    if (!stream)
+        return RAMCRC_EINVAL;
+    HIPCHK(hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)));
+    return RAMCRC_OK;
+}
+
+int ramcrc_ctx_set_cus(ramcrc_ctx* c, int ncu)
+{
+    if (!c || ncu < 0)
+        return RAMCRC_EINVAL;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (ncu == 0 || ncu > c->ncu_all)
+        ncu = c->ncu_all;
+    c->ncu = ncu;
     return RAMCRC_OK;
 }
 

@@ -40,6 +40,12 @@ def lib():
     path = lib_path()
     if not os.path.exists(path):
         raise RamcrcError(f"libramcrc.so not built ({path}); run python -m ramcloud_amd.build")
+    # One HIP runtime per process: torch bundles its own libamdhip64.so.7,
+    # with the same soname as /opt/rocm's, and whichever is loaded first
+    # serves both.  Loading this library first left torch on /opt/rocm's
+    # runtime, which then reported no GPU; importing torch first keeps every
+    # caller on torch's runtime.
+    import torch  # noqa: F401
     L = _c.CDLL(path)
     vp, u32, u64, i32 = _c.c_void_p, _c.c_uint32, _c.c_uint64, _c.c_int
     sig = {
@@ -65,6 +71,9 @@ def lib():
         "ramcrc_ctx_set_timing": (i32, [vp, i32]),
         "ramcrc_ctx_scan_time": (i32, [vp, _c.POINTER(_c.c_double), _c.POINTER(u64)]),
         "ramcrc_ctx_status": (i32, [vp, _c.POINTER(u32)]),
+        "ramcrc_stream_create_cu_mask": (i32, [i32, vp, u32, _c.POINTER(vp)]),
+        "ramcrc_stream_destroy": (i32, [vp]),
+        "ramcrc_ctx_set_cus": (i32, [vp, i32]),
         "ramcrc_strerror": (_c.c_char_p, [i32]),
         "ramcrc_last_hip_error": (i32, []),
         "ramcrc_device_count": (i32, []),
@@ -161,9 +170,37 @@ def _stream(stream):
     if stream is None:
         import torch
         stream = torch.cuda.current_stream()
+    if isinstance(stream, CuMaskStream):
+        return _c.c_void_p(stream.handle)
     if isinstance(stream, int):
         return _c.c_void_p(stream)
     return _c.c_void_p(stream.cuda_stream)
+
+
+class CuMaskStream:
+    """A HIP stream whose kernels run only on the given CUs
+    (ramcrc_stream_create_cu_mask).  Pass it as stream= (it converts to the
+    raw stream handle); destroy() after the work on it has finished."""
+
+    def __init__(self, device, cus):
+        import numpy as np
+        mask = np.zeros(8, np.uint32)
+        for cu in cus:
+            mask[cu // 32] |= np.uint32(1 << (cu % 32))
+        words = int(max(cu for cu in cus) // 32 + 1)
+        h = _c.c_void_p()
+        _check(lib().ramcrc_stream_create_cu_mask(int(device), _c.c_void_p(mask.ctypes.data), words,
+                                                  _c.byref(h)), "ramcrc_stream_create_cu_mask")
+        self.handle = h.value
+        self.ncu = len(set(cus))
+
+    def __int__(self):
+        return self.handle
+
+    def destroy(self):
+        if self.handle:
+            lib().ramcrc_stream_destroy(_c.c_void_p(self.handle))
+            self.handle = None
 
 
 class Context:
@@ -200,6 +237,11 @@ class Context:
         s = _c.c_uint32(0)
         _check(lib().ramcrc_ctx_status(self._h, _c.byref(s)), "ramcrc_ctx_status")
         return s.value
+
+    def set_cus(self, ncu):
+        """Size this context's persistent grids for ncu CUs (0 = all): for
+        launches on a CU-masked stream (see cu_mask_stream)."""
+        _check(lib().ramcrc_ctx_set_cus(self._h, int(ncu)), "ramcrc_ctx_set_cus")
 
     def reserve(self, max_chunks, max_entries):
         _check(lib().ramcrc_ctx_reserve(self._h, max_chunks, max_entries), "ramcrc_ctx_reserve")

@@ -123,3 +123,47 @@ def test_walk_verify_replay_mix(ramcrc, oracle_mod, golden):
               segments.LOG_ENTRY_TYPE_TXDECISION, segments.LOG_ENTRY_TYPE_TXPLIST):
         assert (typ[live] == t).sum() > 10
     assert np.array_equal(c_dev[live], c_exp[live])
+
+
+@pytest.mark.gpu
+def test_walk_verify_on_cu_masked_streams(ramcrc, oracle_mod, golden):
+    """The replay pipeline's plumbing: the walk on one CU-masked stream, the
+    object verify on the complementary mask with a context sized for those
+    CUs (ramcrc_stream_create_cu_mask / ramcrc_ctx_set_cus) give the same
+    status, records and CRCs as the oracle."""
+    import torch
+    buf, certs, bad, _ = segment_cases.build_replay_mix(oracle_mod, golden)
+    nseg, cap = certs.shape[0], segment_cases.CAPACITY
+    exp_status, exp_table, exp_crc = segment_cases.oracle_walk(oracle_mod, buf, certs, nseg)
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    walk_cus = [c for c in range(ncu) if (c // 8) % 4 == 0]
+    rest = [c for c in range(ncu) if (c // 8) % 4 != 0]
+    s_walk, s_scan = ramcrc.CuMaskStream(0, walk_cus), ramcrc.CuMaskStream(0, rest)
+    ctx_walk, ctx_scan = ramcrc.Context(0), ramcrc.Context(0)
+    ctx_scan.set_cus(len(rest))
+    try:
+        d = torch.from_numpy(buf).cuda()
+        dc = torch.from_numpy(np.ascontiguousarray(certs).view(np.int32)).cuda()
+        rv = segments.RecoveryVerify(ctx_scan, nseg, cap, entries_cap=nseg * 4096)
+        torch.cuda.synchronize()
+        ctx_walk.segment_walk(d, rv.stride, rv.capacity, nseg, dc, rv.status, rv.entries,
+                              rv.n_entries, stream=s_walk)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.ExternalStream(s_walk.handle))
+        torch.cuda.ExternalStream(s_scan.handle).wait_event(ev)
+        rv.verify_objects(d, stream=s_scan)
+        torch.cuda.synchronize()
+        status = rv.status.cpu().numpy().view(np.uint32)
+        n = int(rv.n_entries.item())
+        table = rv.entries[:n].cpu().numpy().view(np.uint32)
+        crc = rv.obj_crc[:n].cpu().numpy().view(np.uint32)
+    finally:
+        s_walk.destroy()
+        s_scan.destroy()
+    assert np.array_equal(status, exp_status)
+    assert np.array_equal(status[:, 3], bad)
+    t_dev, c_dev = _sorted(table, crc)
+    t_exp, c_exp = _sorted(exp_table, exp_crc)
+    assert np.array_equal(t_dev, t_exp)
+    live = segment_cases.replay_crc_mask(buf, cap, t_exp)
+    assert np.array_equal(c_dev[live], c_exp[live])
