@@ -134,3 +134,19 @@ def test_oracle_replay_mix(oracle_mod, golden):
     assert (status[:, 0] == segments.SEG_OK).all()
     assert np.array_equal(status[:, 3], bad)
     assert bad.sum() > 0 and (checked > bad).all()
+
+
+def test_walk_cu_split_is_even():
+    """The replay pipeline's walk CUs (bench._walk_cu_list): the same share of
+    every XCD under both CU-id layouts (id % 8 and id // 32)."""
+    import importlib.util
+    import pathlib
+    spec = importlib.util.spec_from_file_location(
+        "bench_mod", pathlib.Path(__file__).resolve().parents[1] / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    for walk in (64, 128):
+        cus = bench._walk_cu_list(256, walk)
+        assert len(set(cus)) == walk and max(cus) < 256
+        assert np.all(np.bincount(np.array(cus) % 8, minlength=8) == walk // 8)
+        assert np.all(np.bincount(np.array(cus) // 32, minlength=8) == walk // 8)
