@@ -66,3 +66,18 @@ def test_shift_and_combine(ramcrc, oracle_mod):
     b = rng.integers(0, 256, 3333, dtype=np.uint8)
     ra, rb = ramcrc.update(0, a), ramcrc.update(0, b)
     assert ramcrc.combine(ra, rb, b.size) == ramcrc.update(0, np.concatenate([a, b]))
+
+
+def test_pipeline_entry_points_reject_bad_arguments(ramcrc):
+    """ramcrc_stream_create_cu_mask / ramcrc_stream_destroy / ramcrc_ctx_set_cus
+    validate their arguments before any HIP call (runs without a GPU)."""
+    import ctypes
+    L = ramcrc.lib()
+    out = ctypes.c_void_p()
+    mask = (ctypes.c_uint32 * 9)(*([0xFFFFFFFF] * 9))
+    assert L.ramcrc_stream_create_cu_mask(0, None, 1, ctypes.byref(out)) == -1
+    assert L.ramcrc_stream_create_cu_mask(0, mask, 0, ctypes.byref(out)) == -1
+    assert L.ramcrc_stream_create_cu_mask(0, mask, 9, ctypes.byref(out)) == -1
+    assert L.ramcrc_stream_create_cu_mask(0, mask, 1, None) == -1
+    assert L.ramcrc_stream_destroy(None) == -1
+    assert L.ramcrc_ctx_set_cus(None, 0) == -1
