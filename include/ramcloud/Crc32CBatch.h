@@ -105,6 +105,30 @@ class Crc32CBatch {
     }
 
     /**
+     * The checks a recovery master makes on a batch of replicas resident in
+     * HBM: Segment::checkMetadataIntegrity of every segment
+     * (src/Segment.cc:758-800), then every checkIntegrity replaySegment makes
+     * on the entries of the segments that passed (src/ObjectManager.cc:580-1100).
+     * Segment i = d_base + i * stride, `capacity` bytes.  d_status[i] gets the
+     * flags, metadata checksum, entry count and failed checks; d_entries /
+     * d_objCrc the walked records and their computed CRCs.  Asynchronous on
+     * `stream`; see ramcrc_segment_walk_device / ramcrc_verify_objects_device.
+     */
+    void
+    deviceReplayVerify(const void* d_base, uint64_t stride, uint32_t capacity, uint64_t count,
+                       const ramcrc_seg_cert* d_certs, ramcrc_seg_status* d_status,
+                       ramcrc_seg_entry* d_entries, uint64_t entriesCap, uint64_t* d_nEntries,
+                       uint32_t* d_objCrc, void* stream = NULL)
+    {
+        check(ramcrc_segment_walk_device(context(), d_base, stride, capacity, count, d_certs,
+                                         d_status, d_entries, entriesCap, d_nEntries, stream),
+              "ramcrc_segment_walk_device");
+        check(ramcrc_verify_objects_device(context(), d_base, stride, d_entries, entriesCap,
+                                           d_nEntries, d_objCrc, d_status, stream),
+              "ramcrc_verify_objects_device");
+    }
+
+    /**
      * Object::assembleForLog's checksum for a batch of serialized objects
      * (the write path, src/ObjectManager.cc:1274): header.checksum of every
      * object (Object::Header + keysAndValue, src/Object.h:137-182) is set to

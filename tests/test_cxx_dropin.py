@@ -64,3 +64,33 @@ def test_cxx_batch_wrapper_gpu(ramcrc, tmp_path):
     out = subprocess.run([str(exe), "gpu"], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "0 mismatches" in out.stdout
+
+
+def _build_replay_test(ramcrc, tmp_path):
+    exe = tmp_path / "replay_test"
+    libdir = os.path.dirname(ramcrc.lib_path())
+    subprocess.check_call([
+        "/opt/rocm/bin/hipcc", "-std=c++17", "-O2", "-Wall", "-Werror",
+        "-I" + os.path.join(ROOT, "tests", "cpp"),
+        "-I" + os.path.join(ROOT, "include", "ramcloud"),
+        "-I" + os.path.join(ROOT, "include"),
+        os.path.join(ROOT, "tests", "cpp", "replay_test.cc"),
+        os.path.join(ROOT, "ramcloud_amd", "dropin", "Crc32C.cc"),
+        "-L" + libdir, "-lramcrc", "-Wl,-rpath," + libdir, "-o", str(exe)])
+    return exe
+
+
+def test_cxx_replay_wrapper_builds(ramcrc, tmp_path):
+    """Crc32CBatch::deviceReplayVerify compiles into a host program (hipcc,
+    for hipMalloc) against the C ABI."""
+    assert _build_replay_test(ramcrc, tmp_path).exists()
+
+
+@pytest.mark.gpu
+def test_cxx_replay_wrapper_gpu(ramcrc, tmp_path):
+    """The C++ replay wrapper on the device: a damaged object counted, a wrong
+    certificate flagged, entries walked in both segments."""
+    exe = _build_replay_test(ramcrc, tmp_path)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "0 mismatches" in out.stdout
