@@ -2073,15 +2073,28 @@ __global__ __launch_bounds__(256) void k_obj_compare(BatchDesc d, ramcrc_seg_sta
     const u32x4 r = d.rec[i];
     const uint32_t type = r.w & 0x3f;
     const uint32_t hdr = replay_header_bytes(type);
-    if (hdr == 0 || !(d.seg_status[r.x].x & RAMCRC_SEG_OK))
+    if (hdr == 0)
+        return;
+    const bool readable = r.z >= hdr && !(r.w & kRecOverlong);
+    const uint64_t payload = reinterpret_cast<uint64_t>(d.base) + uint64_t(r.x) * d.seg_bytes +
+                             r.y + 1 + ((r.w >> 6) & 3) + 1;
+    const gu8* p = reinterpret_cast<const gu8*>(payload);
+    // The segment's status, the stored object checksum and the computed CRC
+    // are independent loads: issue them together (one memory round trip, not
+    // two).  Readable records lie inside their segment, so the object header
+    // read is in bounds.
+    const uint32_t seg_flags = d.seg_status[r.x].x;
+    uint32_t stored = 0, computed = 0;
+    if (type == RAMCRC_LOG_ENTRY_TYPE_OBJ && readable) {
+        stored = le32_g(p);
+        computed = d.out[i];
+    }
+    if (!(seg_flags & RAMCRC_SEG_OK))
         return;
     bool ok = false;
-    if (r.z >= hdr && !(r.w & kRecOverlong)) {
-        const uint64_t payload = reinterpret_cast<uint64_t>(d.base) + uint64_t(r.x) * d.seg_bytes +
-                                 r.y + 1 + ((r.w >> 6) & 3) + 1;
-        const gu8* p = reinterpret_cast<const gu8*>(payload);
+    if (readable) {
         if (type == RAMCRC_LOG_ENTRY_TYPE_OBJ) {
-            ok = d.out[i] == le32_g(p);
+            ok = computed == stored;
         } else {
             // CRC of [0, at) then of [from, from + tail); stored checksum at [at, at + 4)
             uint32_t at = hdr - 4, from = hdr, tail = 0;
