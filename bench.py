@@ -1,35 +1,49 @@
-"""Benchmark: device-resident CRC32C over a batch of 8 MiB segments (BASELINE config 2).
+"""Benchmark of RAMCloud's CRC32C integrity-checksum path on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
                     [--config segments|recovery|entries|stream|replay|append|host]
 
-One step = one pass of the hot path over one batch: ramcrc_segments_device on
-1024 x 8 MiB = 8 GiB of segments already resident in this GPU's HBM (the
-recovery-scan batch, src/BackupMasterRecovery.cc:743-809), plus -- with N > 1
--- the RCCL all-gather of the per-segment CRCs (the only exchange step).
-Weak scaling: every rank owns its own 1024 segments.
+Default (--config segments):
+  N = 1  BASELINE config 2: 1024 x 8 MiB segments resident in HBM, one step =
+         ramcrc_segments_device over the whole 8 GiB batch (the recovery-scan
+         batch, src/BackupMasterRecovery.cc:743-809).
+  N > 1  BASELINE config 4, strong scaling: 2048 x 8 MiB
+         RecoverSegmentBenchmark-shaped object segments
+         (nanobenchmarks/RecoverSegmentBenchmark.cc:123-146) sharded over N
+         GPUs, one step = every rank scans its contiguous range + one RCCL
+         all-gather of the uint32 CRCs (the C-ABI shard entry, ramcrc_shard_*).
+         Rank 0 also times the whole 2048-segment batch alone on its GPU
+         (t1) and reports t1 / tN.
+  `python bench.py --gpus N` with no launcher around it starts N ranks
+  itself (torch.distributed.run, 127.0.0.1) from a process that has made no
+  GPU call; under a launcher WORLD_SIZE must equal N.
 
-Rank 0 prints one JSON line.  `roofline` prices the dominant kernel (k_chunks)
-from its own HIP-event duration on the launch stream; `cpu_baseline` times the
-reference's compiled intelCrc32C (oracle/_ref) -- or the oracle restatement if
-_ref was not shipped -- on a bounded sample of the same segments on this
-host's cores, and checks the GPU CRCs of that sample bit for bit.
+Rank 0 prints one JSON line.  `roofline` prices the dominant kernel from its
+HIP-event duration on its launch stream; `traffic` is the corrected PMC
+FETCH_SIZE of that kernel measured on this exact workload (profiles/pmc/),
+or null when no such profile exists.  `cpu_baseline` (N = 1) times the
+reference's compiled intelCrc32C (oracle/_ref) -- or the oracle restatement
+when _ref was not shipped -- over the same 8 GiB batch on this host's cores
+(1 thread and T = min(physical cores, cgroup CPU quota) threads, best and
+median of 5) and checks every GPU CRC against it.
+
+--host-dry-run runs the N-rank launcher, sharding, host segment fill and the
+result all-gather on the CPU (gloo, libramcrc's host CRC path, no GPU): the
+CPU test of the multi-GPU plumbing.  Its numbers are not GPU measurements.
 """
 import argparse
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
 import numpy as np
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-
-from ramcloud_amd import ramcrc, workloads  # noqa: E402
-from ramcloud_amd.recovery_scan import RecoveryScan, shard_range  # noqa: E402
 
 MiB = 1 << 20
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -40,120 +54,456 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def load_traffic(kernel):
-    """Corrected HBM bytes per launch from the committed PMC summary, if any."""
-    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
+# ------------------------------------------------------------------ launcher
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """Start n ranks of this script (one process per GPU) and return the
+    launcher's exit code.  Runs before anything touches the GPU; the ranks are
+    child processes (no exec), each reading RANK/LOCAL_RANK/WORLD_SIZE."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+# ---------------------------------------------------------------- host facts
+def host_cpu_info():
+    """Logical CPUs, physical cores, sockets, model and the cgroup CPU quota
+    (cpu.max) of this host."""
+    info = {"logical": os.cpu_count() or 1}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        info["affinity"] = info["logical"]
+    cores, sockets, model = set(), set(), None
+    try:
+        phys = core = None
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "physical id":
+                    phys = v
+                elif k == "core id":
+                    core = v
+                elif k == "model name" and model is None:
+                    model = v
+                elif not k and phys is not None:
+                    cores.add((phys, core))
+                    sockets.add(phys)
+                    phys = core = None
+        if phys is not None:
+            cores.add((phys, core))
+            sockets.add(phys)
+    except OSError:
+        pass
+    info["physical_cores"] = len(cores) or info["logical"]
+    info["sockets"] = len(sockets) or 1
+    info["model"] = model
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    info["cgroup_cpu_quota"] = quota
+    return info
+
+
+def baseline_threads(info):
+    t = min(info["physical_cores"], info["affinity"])
+    if info["cgroup_cpu_quota"]:
+        t = min(t, max(1, int(info["cgroup_cpu_quota"])))
+    return max(1, t)
+
+
+# --------------------------------------------------------------- PMC traffic
+def traffic_for(key):
+    """Corrected HBM read bytes per launch of the dominant kernel, measured by
+    rocprofv3 --pmc FETCH_SIZE on exactly this workload (profiles/pmc/<key>.json,
+    written by tools/pmc_traffic.py), or (None, None)."""
+    p = os.path.join(ROOT, "profiles", "pmc", key + ".json")
     try:
         with open(p) as f:
             d = json.load(f)
-        return d[kernel]["hbm_read_bytes_per_launch_corrected"]
-    except Exception:
-        return None
+        return d["hbm_read_bytes_per_launch"], os.path.relpath(p, ROOT)
+    except (OSError, KeyError, ValueError):
+        return None, None
 
 
-def cpu_baseline(host_sample, seg_bytes, nseg_sample, gpu_crcs):
+def roofline(kernel, algo_bytes, kernel_ms, traffic_key):
+    achieved = algo_bytes / (kernel_ms / 1e3) / 1e9 if kernel_ms > 0 else None
+    traffic, src = traffic_for(traffic_key)
+    return {"bound": "hbm", "kernel": kernel,
+            "achieved": round(achieved, 1) if achieved else None,
+            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+            "traffic": traffic, "traffic_source": src,
+            "avg_kernel_ms": round(kernel_ms, 4),
+            "algorithmic_bytes_per_launch": algo_bytes}
+
+
+# ------------------------------------------------------------ distributed
+class Ranks:
+    """RANK/LOCAL_RANK/WORLD_SIZE of this process and the torch.distributed
+    group for barriers, max-over-ranks timing and small host objects."""
+
+    def __init__(self, backend):
+        import torch.distributed as dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = dist
+        self.backend = backend
+        if self.world > 1:
+            if backend == "nccl":
+                import torch
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            else:
+                dist.init_process_group("gloo")
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max(self, x):
+        if self.world == 1:
+            return x
+        import torch
+        dev = "cuda" if self.backend == "nccl" else "cpu"
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def gather_objects(self, obj):
+        if self.world == 1:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def broadcast_object(self, obj):
+        if self.world == 1:
+            return obj
+        box = [obj]
+        self.dist.broadcast_object_list(box, src=0)
+        return box[0]
+
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+def timed(steps, warmup, step, sync, ranks, on_start=None):
+    """W untimed steps, then exactly K steps bracketed by sync + barrier on
+    both sides; returns the slowest rank's seconds.  on_start() runs between
+    the warmup and the timed steps (to reset kernel timers)."""
+    for _ in range(warmup):
+        step()
+    sync()
+    if on_start:
+        on_start()
+    ranks.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    ranks.barrier()
+    return ranks.max(time.perf_counter() - t0)
+
+
+# -------------------------------------------------------------- CPU baselines
+def cpu_baseline_segments(host, seg_bytes, nseg, gpu_crcs, reps=5):
+    """The reference's intelCrc32C (src/Crc32C.h:39-93; oracle/_ref, compiled
+    from /root/reference) over the whole batch, 1 thread and T threads taking
+    whole segments round-robin (RecoverSegmentBenchmark's pool,
+    nanobenchmarks/RecoverSegmentBenchmark.cc:90-118), pinned; best and median
+    of `reps`.  Also the bit-exact check of every GPU CRC."""
     from oracle import oracle
-    kind = "reference" if oracle.ref_available() else "port"
-    use_ref = kind == "reference"
-    try:
-        cpus = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cpus = os.cpu_count() or 1
-    threads = max(1, min(16, cpus))
+    use_ref = oracle.ref_available()
+    info = host_cpu_info()
+    threads = baseline_threads(info)
     res = {}
+    crcs = None
     for t in sorted({1, threads}):
-        best = None
-        crcs = None
-        for _ in range(3):
+        times = []
+        for _ in range(reps):
             t0 = time.perf_counter()
-            crcs = oracle.segments(host_sample, seg_bytes, nseg_sample, threads=t, use_ref=use_ref)
-            dt = time.perf_counter() - t0
-            best = dt if best is None else min(best, dt)
-        res[t] = (nseg_sample * seg_bytes / best / 1e9, crcs)
-    ok = all(np.array_equal(c, gpu_crcs) for _, c in res.values())
-    value, _ = res[threads]
+            crcs = oracle.segments(host, seg_bytes, nseg, threads=t, use_ref=use_ref)
+            times.append(time.perf_counter() - t0)
+        res[t] = (nseg * seg_bytes / min(times) / 1e9, nseg * seg_bytes / statistics.median(times) / 1e9)
+    ok = bool(np.array_equal(crcs, gpu_crcs))
+    best, median = res[threads]
     return {
-        "value": round(value, 3), "unit": "GB/s", "cores": threads, "kind": kind,
-        "sample": f"{nseg_sample} x {seg_bytes // MiB} MiB of the same segments "
-                  f"(first {nseg_sample} of the batch), best of 3, "
-                  f"{'RAMCloud intelCrc32C (src/Crc32C.h:39-93) built -O3 -msse4.2' if use_ref else 'oracle restatement'}, "
-                  f"whole segments round-robin over pinned threads",
+        "value": round(best, 3), "unit": "GB/s", "cores": threads,
+        "kind": "reference" if use_ref else "port",
+        "sample": (f"the whole batch: {nseg} x {seg_bytes // MiB} MiB, best of {reps} "
+                   f"(median {median:.3f} GB/s); "
+                   + ("RAMCloud intelCrc32C (src/Crc32C.h:39-93) compiled -O3 -msse4.2 from the reference"
+                      if use_ref else "oracle restatement of intelCrc32C")
+                   + "; whole segments round-robin over pinned threads"),
+        "median": round(median, 3),
         "single_thread_GBs": round(res[1][0], 3),
-        "host_cpus_visible": cpus,
-        "bit_exact_vs_gpu": bool(ok),
+        "single_thread_median_GBs": round(res[1][1], 3),
+        "threads_rule": "min(physical cores, affinity, cgroup cpu.max quota)",
+        "host": info,
+        "bit_exact_vs_gpu": ok,
     }
 
 
-def run_segments(args, rank, world, local_rank, ctx):
-    seg_bytes = args.seg_mib * MiB
-    if args.config == "recovery":
-        nseg_total = args.nseg_total
-        lo, hi = shard_range(nseg_total, rank, world)
-        nseg = hi - lo
-        first_seed = workloads.SEGMENT_SEED + lo
-        scaling = "strong"
-    else:
-        nseg = args.nseg
-        nseg_total = nseg * world
-        first_seed = workloads.SEGMENT_SEED + rank * nseg
-        scaling = "weak"
-    data = torch.empty(nseg * seg_bytes, dtype=torch.uint8, device="cuda")
-    workloads.splitmix_fill_segments(data, seg_bytes, first_seed)
+def cpu_baseline_entries(host, offs, lens, gpu_crcs, reps=3):
+    """Crc32C::update per entry (the reference's loop of one call per log
+    entry, src/ObjectManager.cc:659-669) restated in the oracle, 1 thread,
+    plus the bit-exact check of every GPU CRC."""
+    from oracle import oracle
+    times = []
+    want = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        want = oracle.entries(host, offs, lens)
+        times.append(time.perf_counter() - t0)
+    total = int(lens.sum())
+    return {"value": round(total / min(times) / 1e9, 3), "unit": "GB/s", "cores": 1,
+            "kind": "port",
+            "sample": f"all {lens.size} entries ({total} B), oracle SSE4.2 restatement of "
+                      f"intelCrc32C, one update per entry, best of {reps}",
+            "bit_exact_vs_gpu": bool(np.array_equal(want, gpu_crcs))}
+
+
+# ------------------------------------------------------------------ configs
+def run_c2(args, ranks):
+    """BASELINE config 2 on each rank's GPU (replicas when run by itself at N > 1
+    with --config c2)."""
+    import torch
+    from ramcloud_amd import ramcrc, workloads
+    ctx = ramcrc.Context(ranks.local)
+    seg = args.seg_mib * MiB
+    nseg = args.nseg
+    data = torch.empty(nseg * seg, dtype=torch.uint8, device="cuda")
+    workloads.splitmix_fill_segments(data, seg, workloads.SEGMENT_SEED)
     out = torch.zeros(nseg, dtype=torch.int32, device="cuda")
-    if args.config == "recovery":
-        scan = RecoveryScan(nseg_total, seg_bytes, rank, world, ctx=ctx)
-    else:
-        scan = RecoveryScan(nseg_total, seg_bytes, rank, world,
-                            scan_fn=lambda d, sb, c, o: ctx.segments(d, sb, c, o))
-        scan.lo, scan.hi = rank * nseg, (rank + 1) * nseg
     torch.cuda.synchronize()
+    ctx.set_timing(True)
+    elapsed = timed(args.steps, args.warmup, lambda: ctx.segments(data, seg, nseg, out),
+                    torch.cuda.synchronize, ranks, on_start=ctx.scan_time)
+    kernel_ms, launches = ctx.scan_time()
+    ctx.set_timing(False)
+    avg_ms = kernel_ms / max(launches, 1)
+    gpu = out.cpu().numpy().view(np.uint32)
+    kat_ok = None
+    if ranks.rank == 0:
+        with open(os.path.join(ROOT, "tests", "golden", "crc32c_golden.json")) as f:
+            kats = {k["name"]: k["crc"] for k in json.load(f)["kat"] if "crc" in k}
+        kat_ok = all(int(gpu[i]) == kats[f"bench_segment_{i}"] for i in range(min(4, nseg)))
+    line = None
+    if ranks.rank == 0:
+        cpu = None
+        if ranks.world == 1 and not args.no_cpu_baseline:
+            host = data.cpu().numpy()
+            cpu = cpu_baseline_segments(host, seg, nseg, gpu, reps=args.cpu_reps)
+        key = f"c2_{nseg}x{args.seg_mib}MiB_k_chunks"
+        line = {
+            "metric": METRIC,
+            "value": round(ranks.world * nseg * seg * args.steps / elapsed / 1e9, 2),
+            "unit": "GB/s", "n_gpus": ranks.world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong" if ranks.world == 1 else "weak",
+            "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (splitmix64 bytes, seed 0x52414D43+i per segment)",
+            "config": {"workload": f"{nseg} x {args.seg_mib} MiB device-resident segments "
+                                   "(BASELINE config 2)" + (" per GPU" if ranks.world > 1 else ""),
+                       "segments_per_gpu": nseg, "segment_bytes": seg,
+                       "batch_bytes_per_gpu": nseg * seg,
+                       "parallelism": "single" if ranks.world == 1 else f"replicas{ranks.world}",
+                       "exchange": "none"},
+            "roofline": roofline("k_chunks", nseg * seg, avg_ms, key),
+            "cpu_baseline": cpu,
+            "bit_exact_kat": kat_ok,
+        }
+        if ranks.world == 1:
+            line["scaling_note"] = ("N=1 runs BASELINE config 2 (1024 segments); N>1 runs config 4 "
+                                    "(2048 segments sharded, strong scaling); value is GB/s in both")
+    ctx.close()
+    return line
 
-    def step():
-        return scan.step(data, out)
 
+def _fill_recovery_shard(ctx, data, seg, lo, count, value_len, certs=None):
+    """Segments lo .. lo+count-1 of the C4 batch: splitmix64 value bytes (seed
+    0x52414D43 + i), then RecoverSegmentBenchmark's objects with keys
+    continuing across segments (first key of segment i = i * per), built on
+    the device (ramcrc_segment_fill_objects_device).  Returns (objects per
+    segment, certificate length, certificate checksum)."""
+    from ramcloud_amd import segments, workloads
+    per = segments.objects_per_segment(seg, value_len)
+    if count:
+        workloads.splitmix_fill_segments(data, seg, workloads.SEGMENT_SEED + lo)
+    got, length, ck = ctx.fill_objects(data, seg, seg, count, value_len, first_key=lo * per,
+                                       certs=certs)
+    assert got == per, (got, per)
+    return per, length, ck
+
+
+def run_recovery(args, ranks):
+    """BASELINE config 4: the recovery-scan shard, strong scaling."""
+    import torch
+    from ramcloud_amd import ramcrc
+    seg = args.seg_mib * MiB
+    total = args.nseg_total
+    lo, hi = ramcrc.shard_range(total, ranks.world, ranks.rank)
+    count = hi - lo
+    setup = ramcrc.Context(ranks.local)
+    data = torch.empty(max(count, 1) * seg, dtype=torch.uint8, device="cuda")
+    per, _, _ = _fill_recovery_shard(setup, data, seg, lo, count, args.value_len)
+    # spot check of the placement: each rank's first segment through the
+    # host CRC path, compared after the gather
+    mine = (lo, ramcrc.crc32c(data[:seg].cpu().numpy())) if count else None
+    uid = ranks.broadcast_object(ramcrc.shard_unique_id() if ranks.rank == 0 else None)
+    shard = ramcrc.Shard(uid=uid, nranks=ranks.world, rank=ranks.rank, device=ranks.local)
+    out = torch.zeros(total, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    shard.set_timing(True)
+
+    def sync():
+        shard.sync()
+        torch.cuda.synchronize()
+
+    elapsed = timed(args.steps, args.warmup, lambda: shard.segments([data], seg, total, outs=[out]),
+                    sync, ranks, on_start=shard.scan_time)
+    kernel_ms, launches = shard.scan_time()
+    shard.set_timing(False)
+    avg_ms = kernel_ms / max(launches, 1)
+    gathered = out.cpu().numpy().view(np.uint32)
+    checks = ranks.gather_objects(mine)
+    spot_ok = all(c is None or int(gathered[c[0]]) == c[1] for c in checks)
+    shard.close()
+    del data
+    torch.cuda.empty_cache()
+    ranks.barrier()
+    t1 = None
+    if ranks.rank == 0 and ranks.world > 1 and not args.no_t1:
+        t1 = _recovery_t1(args, ranks, setup)
+    ranks.barrier()
+    setup.close()
+    if ranks.rank != 0:
+        return None
+    tn_ms = elapsed / args.steps * 1e3
+    key = f"c4_{total}x{args.seg_mib}MiB_v{args.value_len}_n{ranks.world}_k_chunks"
+    line = {
+        "metric": METRIC,
+        "value": round(total * seg * args.steps / elapsed / 1e9, 2),
+        "unit": "GB/s", "n_gpus": ranks.world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(tn_ms, 4), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "u8",
+        "data": ("synthetic RecoverSegmentBenchmark-shaped object segments "
+                 f"({per} objects of {args.value_len} B values per segment, splitmix64 value "
+                 "bytes seed 0x52414D43+i, keys continuing across segments)"),
+        "config": {"workload": f"recovery scan (BASELINE config 4): {total} x {args.seg_mib} MiB "
+                               f"segments sharded over {ranks.world} GPUs",
+                   "segments_total": total, "segments_per_gpu_max": (total + ranks.world - 1) // ranks.world,
+                   "segment_bytes": seg, "parallelism": f"shard{ranks.world}",
+                   "exchange": "RCCL ncclAllGather of uint32 CRCs (libramcrc ramcrc_shard_segments)"},
+        "roofline": roofline("k_chunks", count * seg, avg_ms, key),
+        "bit_exact_spot_check": bool(spot_ok),
+    }
+    if t1 is not None:
+        line["t1_ms"] = round(t1, 4)
+        line["speedup_t1_over_tN"] = round(t1 / tn_ms, 3)
+    return line
+
+
+def _recovery_t1(args, ranks, ctx):
+    """The whole C4 batch on rank 0's GPU alone (a 1-rank shard), same steps."""
+    import torch
+    from ramcloud_amd import ramcrc
+    seg = args.seg_mib * MiB
+    total = args.nseg_total
+    data = torch.empty(total * seg, dtype=torch.uint8, device="cuda")
+    _fill_recovery_shard(ctx, data, seg, 0, total, args.value_len)
+    solo = ramcrc.Shard(uid=ramcrc.shard_unique_id(), nranks=1, rank=0, device=ranks.local)
+    out = torch.zeros(total, dtype=torch.int32, device="cuda")
+    step = lambda: solo.segments([data], seg, total, outs=[out])  # noqa: E731
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    ctx.set_timing(True)
-    ctx.scan_time()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    solo.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        full = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    scan_ms, launches = ctx.scan_time()
-    ctx.set_timing(False)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    gpu_crcs = full.cpu().numpy().view(np.uint32) if world > 1 else out.cpu().numpy().view(np.uint32)
-    local_crcs = out.cpu().numpy().view(np.uint32)
-    return dict(seg_bytes=seg_bytes, nseg=nseg, nseg_total=nseg_total, elapsed=elapsed,
-                scan_ms=scan_ms, launches=launches, data=data, local_crcs=local_crcs,
-                all_crcs=gpu_crcs, first_seed=first_seed, scaling=scaling)
+        step()
+    solo.sync()
+    t1 = (time.perf_counter() - t0) / args.steps * 1e3
+    solo.close()
+    del data
+    torch.cuda.empty_cache()
+    return t1
 
 
-def max_over_ranks(elapsed, world):
-    """Whole-job time: the slowest rank's timed region."""
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    return elapsed
+def run_recovery_host_dry(args, ranks):
+    """The N-rank plumbing of config 4 on the CPU: the same launcher, shard
+    ranges, object fill (host append path) and result all-gather (gloo), with
+    libramcrc's host CRC path as the per-segment scan.  No GPU numbers."""
+    import torch
+    from ramcloud_amd import ramcrc, segments, workloads
+    from ramcloud_amd.recovery_scan import RecoveryScan
+    seg = args.seg_kib * 1024 if args.seg_kib else args.seg_mib * MiB
+    total = args.nseg_total
+    per = segments.objects_per_segment(seg, args.value_len)
+
+    def scan_fn(shard, seg_bytes, count, out):
+        a = shard.numpy()
+        for j in range(count):
+            out[j] = int(np.uint32(ramcrc.crc32c(a[j * seg_bytes:(j + 1) * seg_bytes])).view(np.int32))
+
+    scan = RecoveryScan(total, seg, ranks.rank, ranks.world, scan_fn=scan_fn)
+    shard = torch.empty(max(scan.count, 1) * seg, dtype=torch.uint8)
+    a = shard.numpy()
+    for i in range(scan.lo, scan.hi):
+        s = a[(i - scan.lo) * seg:(i - scan.lo + 1) * seg]
+        s[:] = workloads.splitmix_bytes_np(workloads.SEGMENT_SEED + i, seg)
+        ramcrc.segment_fill_objects(s, args.value_len, first_key=i * per)
+    out = torch.zeros(max(scan.count, 1), dtype=torch.int32)
+    box = {}
+
+    def step():
+        box["full"] = scan.step(shard, out)
+
+    elapsed = timed(args.steps, args.warmup, step, lambda: None, ranks)
+    if ranks.rank != 0:
+        return None
+    crcs = box["full"].numpy().view(np.uint32)
+    return {
+        "metric": METRIC + " [host dry run: CPU plumbing test, not a GPU measurement]",
+        "value": round(total * seg * args.steps / elapsed / 1e9, 4), "unit": "GB/s",
+        "n_gpus": ranks.world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic RecoverSegmentBenchmark-shaped object segments (host dry run)",
+        "config": {"workload": f"recovery scan: {total} x {seg} B segments sharded over "
+                               f"{ranks.world} ranks", "segments_total": total,
+                   "segment_bytes": seg, "value_len": args.value_len,
+                   "parallelism": f"shard{ranks.world}", "exchange": "gloo all_gather (dry run)"},
+        "dry_run": True,
+        "crcs": [int(c) for c in crcs] if total <= 256 else None,
+        "crc_of_crcs": ramcrc.crc32c(np.ascontiguousarray(crcs)),
+    }
 
 
-def run_entries(args, ctx, world=1):
-    """Config 3. The small-entry batch does not shard: at N>1
-    every rank runs an independent replica of the same 1M-entry batch, and the
-    job value is N x bytes / the slowest rank's time (weak scaling)."""
+def run_entries(args, ranks):
+    """Config 3: 1 M mixed log entries; replicas at N > 1."""
+    import torch
+    from ramcloud_amd import ramcrc, workloads
+    ctx = ramcrc.Context(ranks.local)
     lens = workloads.entry_lengths(args.entries)
     if args.entry_size:
         lens = lens * 0 + np.uint64(args.entry_size)
@@ -166,73 +516,58 @@ def run_entries(args, ctx, world=1):
     len_t = torch.from_numpy(lens.view(np.int64)).cuda()
     out = torch.zeros(lens.size, dtype=torch.int32, device="cuda")
     fn = ctx.entries if args.path == "entries" else ctx.batch
-    for _ in range(args.warmup):
-        fn(data, off_t, len_t, out)
     torch.cuda.synchronize()
     ctx.set_timing(True)
-    ctx.scan_time()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        fn(data, off_t, len_t, out)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = max_over_ranks(time.perf_counter() - t0, world)
-    scan_ms, launches = ctx.scan_time()
+    elapsed = timed(args.steps, args.warmup, lambda: fn(data, off_t, len_t, out),
+                    torch.cuda.synchronize, ranks, on_start=ctx.scan_time)
+    kernel_ms, _ = ctx.scan_time()
     ctx.set_timing(False)
-    return dict(total=total, n=lens.size, elapsed=elapsed, scan_ms=scan_ms, launches=launches,
-                host=host, offs=offs, lens=lens, crcs=out.cpu().numpy().view(np.uint32))
+    ctx.check()
+    if ranks.rank != 0:
+        ctx.close()
+        return None
+    gpu = out.cpu().numpy().view(np.uint32)
+    cpu = None if args.no_cpu_baseline else cpu_baseline_entries(host, offs, lens, gpu)
+    scan_ms = kernel_ms / args.steps
+    mix = "fixed %d B" % args.entry_size if args.entry_size else "100B/1KiB/4KiB Zipf"
+    key = f"c3_{lens.size}_{'mix' if not args.entry_size else args.entry_size}_{args.path}"
+    ctx.close()
+    return {
+        "metric": f"device-resident CRC32C GB/s over {lens.size} log entries ({mix})",
+        "value": round(ranks.world * total * args.steps / elapsed / 1e9, 2), "unit": "GB/s",
+        "n_gpus": ranks.world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": f"{lens.size} entries, {total} bytes per GPU (BASELINE config 3)",
+                   "path": args.path,
+                   "parallelism": f"replicas{ranks.world}" if ranks.world > 1 else "single",
+                   "exchange": "none", "table_bytes_not_credited": 16 * lens.size},
+        "roofline": dict(roofline("k_entries_tiny+k_entries" if args.path == "entries"
+                                  else "k_chunks+k_entries_tiny+k_entries", total, scan_ms, key),
+                         scan_ms_per_step=round(scan_ms, 4)),
+        "cpu_baseline": cpu,
+    }
 
 
-def run_replay(args, ctx):
-    """Recovery replay verify (RecoverSegmentBenchmark-shaped,
-    nanobenchmarks/RecoverSegmentBenchmark.cc:123-146): nseg 8 MiB segments
-    full of objects with 8-byte counter keys and value_len-byte values, built
-    by the host append path; one step = Segment::checkMetadataIntegrity of
-    every segment (src/Segment.cc:758-800) + Object::computeChecksum of every
-    object compared with its stored checksum (src/ObjectManager.cc:659-669)."""
-    from ramcloud_amd import segments
-    seg_bytes = args.seg_mib * MiB
-    nseg = args.replay_nseg
-    # value bytes: splitmix64 streams generated on the device, objects
-    # appended on the host (C append path, threads), copied back
-    d = torch.empty(nseg * seg_bytes, dtype=torch.uint8, device="cuda")
-    workloads.splitmix_fill_segments(d, seg_bytes, segments.REPLAY_SEED)
-    host = d.cpu().numpy()
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    certs, counts = segments.fill_segments_host(host, nseg, seg_bytes, args.value_len,
-                                                threads=threads)
-    d.copy_(torch.from_numpy(host))
-    dc = torch.from_numpy(np.ascontiguousarray(certs).view(np.int32)).cuda()
-    cap = int(counts.sum()) + nseg
-    if args.walk_cus:
-        elapsed, scan_ms, launches, sts = _replay_pipelined(args, ctx, d, dc, nseg, seg_bytes, cap)
-    else:
-        rv = segments.RecoveryVerify(ctx, nseg, seg_bytes, entries_cap=cap)
-        for _ in range(args.warmup):
-            rv.verify(d, dc)
-        torch.cuda.synchronize()
-        ctx.set_timing(True)
-        ctx.scan_time()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            st = rv.verify(d, dc)
-        torch.cuda.synchronize()
-        elapsed = time.perf_counter() - t0
-        scan_ms, launches = ctx.scan_time()
-        ctx.set_timing(False)
-        sts = [st]
-    ok = True
-    for st in sts:
-        status = st.cpu().numpy().view(np.uint32)
-        ok = ok and bool((status[:, 0] == segments.SEG_OK).all() and (status[:, 3] == 0).all()
-                         and np.array_equal(status[:, 2], counts)
-                         and np.array_equal(status[:, 1], certs[:, 1]))
-    return dict(seg_bytes=seg_bytes, nseg=nseg, counts=counts, certs=certs, host=host,
-                elapsed=elapsed, scan_ms=scan_ms, launches=launches, ok=ok)
+def replay_cpu_baseline(host, seg_bytes, certs, nsample):
+    """The restated reference walk + per-object verify (oracle, SSE4.2 CRC) on
+    nsample segments, one thread -- the checksum work of one
+    RecoverSegmentBenchmark replay thread."""
+    from oracle import oracle
+    t0 = time.perf_counter()
+    bad = 0
+    for i in range(nsample):
+        s = host[i * seg_bytes:(i + 1) * seg_bytes]
+        f, ck, n, table = oracle.check_metadata(s, int(certs[i, 0]), int(certs[i, 1]),
+                                                segment=0, table_cap=seg_bytes // 14 + 1)
+        b, _, _ = oracle.verify_objects(s, seg_bytes, table, 1)
+        bad += b + (0 if f == 1 else 1)
+    dt = time.perf_counter() - t0
+    return {"value": round(nsample * seg_bytes / dt / 1e9, 3), "unit": "GB/s", "cores": 1,
+            "kind": "port",
+            "sample": f"{nsample} x {seg_bytes // MiB} MiB object segments, oracle restatement of "
+                      "Segment::checkMetadataIntegrity + Object::computeChecksum, 1 thread",
+            "all_verified": bad == 0}
 
 
 def _walk_cu_list(ncu, walk_cus):
@@ -252,6 +587,7 @@ def _replay_pipelined(args, ctx, d, dc, nseg, seg_bytes, cap):
     is a copy of the first at another HBM address.  Every timed step walks and
     verifies exactly one whole batch: the first walk and the last scan are
     inside the timed region."""
+    import torch
     from ramcloud_amd import ramcrc, segments
     dev = torch.cuda.current_device()
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -301,6 +637,8 @@ def _replay_pipelined(args, ctx, d, dc, nseg, seg_bytes, cap):
     elapsed = time.perf_counter() - t0
     scan_ms, launches = ctx.scan_time()
     ctx.set_timing(False)
+    for rv in rvs:
+        rv.check()
     sts = [rv.status.clone() for rv in rvs]
     ctx.set_cus(0)
     ctx_walk.close()
@@ -309,12 +647,86 @@ def _replay_pipelined(args, ctx, d, dc, nseg, seg_bytes, cap):
     return elapsed, scan_ms, launches, sts
 
 
-def run_append(args, ctx):
+def run_replay(args, ranks):
+    """Recovery replay verify (RecoverSegmentBenchmark-shaped,
+    nanobenchmarks/RecoverSegmentBenchmark.cc:123-146): nseg 8 MiB segments
+    full of objects with 8-byte counter keys and value_len-byte values; one
+    step = Segment::checkMetadataIntegrity of every segment
+    (src/Segment.cc:758-800) + Object::computeChecksum of every object
+    compared with its stored checksum (src/ObjectManager.cc:659-669)."""
+    import torch
+    from ramcloud_amd import ramcrc, segments
+    ctx = ramcrc.Context(ranks.local)
+    seg = args.seg_mib * MiB
+    nseg = args.replay_nseg
+    d = torch.empty(nseg * seg, dtype=torch.uint8, device="cuda")
+    certs_t = torch.zeros((nseg, 2), dtype=torch.int32, device="cuda")
+    per, _, _ = _fill_recovery_shard(ctx, d, seg, 0, nseg, args.value_len, certs=certs_t)
+    certs = certs_t.cpu().numpy().view(np.uint32)
+    counts = np.full(nseg, per, np.uint32)
+    cap = int(counts.sum()) + nseg
+    if args.walk_cus:
+        elapsed, scan_ms, launches, sts = _replay_pipelined(args, ctx, d, certs_t, nseg, seg, cap)
+    else:
+        rv = segments.RecoveryVerify(ctx, nseg, seg, entries_cap=cap)
+        torch.cuda.synchronize()
+        ctx.set_timing(True)
+        box = {}
+
+        def step():
+            box["st"] = rv.verify(d, certs_t)
+
+        elapsed = timed(args.steps, args.warmup, step, torch.cuda.synchronize, ranks,
+                        on_start=ctx.scan_time)
+        scan_ms, launches = ctx.scan_time()
+        ctx.set_timing(False)
+        rv.check()
+        sts = [box["st"]]
+    ok = True
+    for st in sts:
+        status = st.cpu().numpy().view(np.uint32)
+        ok = ok and bool((status[:, 0] == segments.SEG_OK).all() and (status[:, 3] == 0).all()
+                         and np.array_equal(status[:, 2], counts)
+                         and np.array_equal(status[:, 1], certs[:, 1]))
+    obj_bytes = int(counts.sum()) * (segments.OBJECT_OVERHEAD + args.value_len - 4)
+    cpu = None
+    if not args.no_cpu_baseline:
+        ns = min(args.replay_cpu_sample, nseg)
+        cpu = replay_cpu_baseline(d[:ns * seg].cpu().numpy(), seg, certs, ns)
+    ctx.close()
+    scan_s = scan_ms / args.steps / 1e3
+    achieved = obj_bytes / scan_s / 1e9 if scan_s > 0 else None
+    return {
+        "metric": "device-resident recovery replay verify GB/s of 8 MiB object segments "
+                  "(segment walk + per-object checksum compare)",
+        "value": round(nseg * seg * args.steps / elapsed / 1e9, 2), "unit": "GB/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (RecoverSegmentBenchmark-shaped objects, splitmix64 values)",
+        "config": {"workload": f"{nseg} x {args.seg_mib} MiB segments of "
+                               f"{args.value_len} B-value objects",
+                   "pipeline": (f"walk on {args.walk_cus} CUs beside the scan of the previous batch"
+                                if args.walk_cus else "none"),
+                   "objects": int(counts.sum()), "object_bytes_checksummed": obj_bytes},
+        "roofline": {"bound": "hbm", "kernel": "k_entries (object verify)",
+                     "achieved": round(achieved, 1) if achieved else None,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                     "traffic": None, "scan_ms_per_step": round(scan_s * 1e3, 4)},
+        "cpu_baseline": cpu,
+        "all_segments_verified": ok,
+    }
+
+
+def run_append(args, ranks):
     """Batched write-path checksum (SURVEY.md 8(f) row 4): Object::assembleForLog
     (src/Object.cc:213-238) over a batch of 1M serialized objects of the
     config-3 sizes (100 B / 1 KiB / 4 KiB, Zipf), packed back to back in HBM;
     one step = every header.checksum computed and stamped."""
-    from oracle import oracle
+    import torch
+    from ramcloud_amd import ramcrc, workloads
+    ctx = ramcrc.Context(ranks.local)
     lens = workloads.entry_lengths(args.entries)
     offs = workloads.packed_offsets(lens)
     total = int(lens.sum())
@@ -323,49 +735,79 @@ def run_append(args, ctx):
     off_t = torch.from_numpy(offs.view(np.int64)).cuda()
     len_t = torch.from_numpy(lens.view(np.int64)).cuda()
     out = torch.zeros(lens.size, dtype=torch.int32, device="cuda")
-    for _ in range(args.warmup):
-        ctx.assemble_objects(data, off_t, len_t, out)
     torch.cuda.synchronize()
     ctx.set_timing(True)
-    ctx.scan_time()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ctx.assemble_objects(data, off_t, len_t, out)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed(args.steps, args.warmup, lambda: ctx.assemble_objects(data, off_t, len_t, out),
+                    torch.cuda.synchronize, ranks, on_start=ctx.scan_time)
     scan_ms, _ = ctx.scan_time()
     ctx.set_timing(False)
+    ctx.check()
     credited = total - 4 * lens.size   # bytes [4, len) of every object
-    want = oracle.entries(host, offs + 4, lens - 4)
     got = out.cpu().numpy().view(np.uint32)
     stamped = data.cpu().numpy()
     hdr = stamped[(offs.astype(np.int64)[:, None] + np.arange(4)).reshape(-1)].reshape(-1, 4).copy().view("<u4")[:, 0]
-    ok = bool(np.array_equal(got, want) and np.array_equal(hdr, want))
-    value = credited * args.steps / elapsed / 1e9
+    cpu = None
+    if not args.no_cpu_baseline:
+        cpu = cpu_baseline_entries(host, offs + 4, lens - 4, got, reps=1)
+        cpu["stamped_headers_match"] = bool(np.array_equal(hdr, got))
+        cpu["sample"] += " (object bytes [4, len))"
+    ctx.close()
     scan_s = scan_ms / args.steps / 1e3
     achieved = credited / scan_s / 1e9 if scan_s > 0 else None
     return {
         "metric": "device-resident Object::assembleForLog checksum GB/s over 1M objects "
                   "(100B/1KiB/4KiB Zipf)",
-        "value": round(value, 2), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-        "data": "synthetic", "config": {"workload": f"{lens.size} objects, {total} bytes",
-                                        "credited_bytes": credited},
+        "value": round(credited * args.steps / elapsed / 1e9, 2), "unit": "GB/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": f"{lens.size} objects, {total} bytes", "credited_bytes": credited},
         "roofline": {"bound": "hbm", "kernel": "k_entries",
                      "achieved": round(achieved, 1) if achieved else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                      "traffic": None, "scan_ms_per_step": round(scan_s * 1e3, 4)},
-        "bit_exact_vs_oracle": ok,
+        "cpu_baseline": cpu,
     }
+
+
+def run_stream(args, ranks):
+    """Config 5: pinned host segments streamed through the GPU (H2D on a copy
+    stream overlapped with the kernels), CRCs back to host: host-to-host."""
+    import torch
+    from ramcloud_amd import ramcrc, workloads
+    ctx = ramcrc.Context(ranks.local)
+    seg = args.seg_mib * MiB
+    nseg = args.nseg
+    host = torch.empty(nseg * seg, dtype=torch.uint8).pin_memory()
+    dev = torch.empty(nseg * seg, dtype=torch.uint8, device="cuda")
+    workloads.splitmix_fill_segments(dev, seg, workloads.SEGMENT_SEED)
+    host.copy_(dev)
+    del dev
+    torch.cuda.synchronize()
+    box = {}
+
+    def step():
+        box["out"] = ctx.stream_host(host, seg, nseg, batch=8, depth=3)
+
+    elapsed = timed(args.steps, 1, step, lambda: None, ranks)
+    out = box["out"]
+    a = host.numpy()
+    spot = all(int(out[i]) == ramcrc.crc32c(a[i * seg:(i + 1) * seg]) for i in range(min(4, nseg)))
+    ctx.close()
+    return {"metric": "host-to-host streamed CRC32C GB/s (pinned H2D overlapped)",
+            "value": round(nseg * seg * args.steps / elapsed / 1e9, 2), "unit": "GB/s",
+            "n_gpus": 1, "steps": args.steps, "warmup": 1,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": f"{nseg} x {args.seg_mib} MiB pinned host segments"},
+            "bit_exact_spot_check_host_path": bool(spot)}
 
 
 def run_host():
     """The synchronous host path Crc32C::update now calls (no GPU), timed
     beside the reference's own intelCrc32C (oracle/_ref, the CPU baseline) by
     tools/bin/host_bench in the shape of src/misc/crc32c.cc:57-104."""
-    import subprocess
     exe = os.path.join(ROOT, "tools", "bin", "host_bench")
     ref = os.path.join(ROOT, "oracle", "_ref", "libref_crc32c.so")
     if not os.path.exists(exe):
@@ -391,211 +833,77 @@ def run_host():
     }
 
 
-def replay_cpu_baseline(host, seg_bytes, certs, nsample):
-    """The restated reference walk + per-object verify (oracle, SSE4.2 CRC) on
-    nsample segments, one thread -- the checksum work of one
-    RecoverSegmentBenchmark replay thread."""
-    from oracle import oracle
-    t0 = time.perf_counter()
-    bad = 0
-    for i in range(nsample):
-        seg = host[i * seg_bytes:(i + 1) * seg_bytes]
-        f, ck, n, table = oracle.check_metadata(seg, int(certs[i, 0]), int(certs[i, 1]),
-                                                segment=0, table_cap=seg_bytes // 36 + 1)
-        b, _, _ = oracle.verify_objects(seg, seg_bytes, table, 1)
-        bad += b + (0 if f == 1 else 1)
-    dt = time.perf_counter() - t0
-    return {"value": round(nsample * seg_bytes / dt / 1e9, 3), "unit": "GB/s", "cores": 1,
-            "kind": "port",
-            "sample": f"{nsample} x {seg_bytes // MiB} MiB object segments, oracle restatement of "
-                      "Segment::checkMetadataIntegrity + Object::computeChecksum, 1 thread",
-            "all_verified": bad == 0}
-
-
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks); default WORLD_SIZE or 1")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="segments",
-                    choices=["segments", "recovery", "entries", "stream", "replay", "append",
-                             "host"])
-    ap.add_argument("--nseg", type=int, default=1024, help="segments per GPU (weak scaling)")
-    ap.add_argument("--nseg-total", type=int, default=2048, help="recovery config: total segments")
+                    choices=["segments", "c2", "recovery", "entries", "stream", "replay", "append",
+                             "host"],
+                    help="segments: config 2 at N=1, config 4 (recovery) at N>1")
+    ap.add_argument("--nseg", type=int, default=1024, help="config 2/5: segments per GPU")
+    ap.add_argument("--nseg-total", type=int, default=2048, help="config 4: segments in the batch")
     ap.add_argument("--seg-mib", type=int, default=8)
+    ap.add_argument("--seg-kib", type=int, default=0, help="--host-dry-run: segment KiB")
+    ap.add_argument("--value-len", type=int, default=1024,
+                    help="config 4 / replay: object value bytes (RecoverSegmentBenchmark default)")
     ap.add_argument("--entries", type=int, default=1_000_000)
     ap.add_argument("--path", default="entries", choices=["entries", "batch"])
     ap.add_argument("--entry-size", type=int, default=0, help="fixed entry length (default: Zipf mix)")
     ap.add_argument("--replay-nseg", type=int, default=512,
                     help="replay config: segments (RecoverSegmentBenchmark: 4096/8)")
-    ap.add_argument("--value-len", type=int, default=1024, help="replay config: object value bytes")
-    ap.add_argument("--cpu-sample", type=int, default=128, help="segments timed on the CPU")
     ap.add_argument("--replay-cpu-sample", type=int, default=16,
                     help="replay config: segments verified by the CPU baseline")
     ap.add_argument("--walk-cus", type=int, default=0,
                     help="replay config: pipeline batches, walking on this many CUs "
                          "(a multiple of 8) beside the object scan on the rest; 0 = serial")
+    ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    args = ap.parse_args()
+    ap.add_argument("--no-t1", action="store_true", help="config 4 at N>1: skip the 1-GPU t1 run")
+    ap.add_argument("--host-dry-run", action="store_true",
+                    help="config 4 plumbing on the CPU (gloo, host CRC path, no GPU)")
+    return ap.parse_args(argv)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+def main():
+    args = parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    n = args.gpus if args.gpus is not None else int(env_world or 1)
+    if n < 1:
+        log("bench: --gpus must be >= 1")
+        return 2
+    if env_world is None and n > 1:
+        return launch_ranks(n, sys.argv[1:])   # before any GPU call
+    if int(env_world or 1) != n:
+        log(f"bench: --gpus {n} but the launcher started WORLD_SIZE={env_world} ranks")
+        return 2
+
+    from ramcloud_amd import ramcrc
     ramcrc.lib()  # fail loudly if the HIP library is missing
     if args.config == "host":
         print(json.dumps(run_host()), flush=True)
-        return
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    ctx = ramcrc.Context(local_rank)
-
-    if args.config in ("segments", "recovery"):
-        r = run_segments(args, rank, world, local_rank, ctx)
-        total_bytes = r["nseg_total"] * r["seg_bytes"] * args.steps
-        value = total_bytes / r["elapsed"] / 1e9
-        avg_scan_s = r["scan_ms"] / max(r["launches"], 1) / 1e3
-        bytes_per_launch = r["nseg"] * r["seg_bytes"]
-        achieved = bytes_per_launch / avg_scan_s / 1e9 if avg_scan_s > 0 else None
-        # correctness of this run: known answers for the first segments
-        kat_ok = None
-        if rank == 0 and r["first_seed"] == workloads.SEGMENT_SEED:
-            with open(os.path.join(ROOT, "tests", "golden", "crc32c_golden.json")) as f:
-                kats = {k["name"]: k["crc"] for k in json.load(f)["kat"] if "crc" in k}
-            kat_ok = all(int(r["local_crcs"][i]) == kats[f"bench_segment_{i}"]
-                         for i in range(min(4, r["nseg"])))
-        line = None
-        if rank == 0:
-            cpu = None
-            if world == 1 and not args.no_cpu_baseline:
-                ns = min(args.cpu_sample, r["nseg"])
-                sample = r["data"][: ns * r["seg_bytes"]].cpu().numpy()
-                cpu = cpu_baseline(sample, r["seg_bytes"], ns, r["local_crcs"][:ns])
-            line = {
-                "metric": METRIC,
-                "value": round(value, 2),
-                "unit": "GB/s",
-                "n_gpus": world,
-                "steps": args.steps,
-                "warmup": args.warmup,
-                "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 4),
-                "higher_is_better": True,
-                "scaling": r["scaling"],
-                "vs_baseline": None,
-                "dtype": "u8",
-                "data": "synthetic (splitmix64 bytes, seed 0x52414D43+i per segment)",
-                "config": {
-                    "workload": ("recovery scan: %d x %d MiB segments sharded over %d GPUs"
-                                 % (r["nseg_total"], args.seg_mib, world))
-                    if args.config == "recovery" else
-                    ("%d x %d MiB device-resident segments per GPU (BASELINE config 2)"
-                     % (r["nseg"], args.seg_mib)),
-                    "segments_per_gpu": r["nseg"],
-                    "segment_bytes": r["seg_bytes"],
-                    "batch_bytes_per_gpu": r["nseg"] * r["seg_bytes"],
-                    "parallelism": f"shard{world}" if world > 1 else "single",
-                    "exchange": "rccl all_gather of uint32 CRCs" if world > 1 else "none",
-                },
-                "roofline": {
-                    "bound": "hbm",
-                    "kernel": "k_chunks",
-                    "achieved": round(achieved, 1) if achieved else None,
-                    "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                    "traffic": load_traffic("k_chunks"),
-                    "avg_kernel_ms": round(avg_scan_s * 1e3, 4),
-                    "algorithmic_bytes_per_launch": bytes_per_launch,
-                },
-                "cpu_baseline": cpu,
-                "bit_exact_kat": kat_ok,
-            }
-    elif args.config == "entries":
-        r = run_entries(args, ctx, world)
-        value = world * r["total"] * args.steps / r["elapsed"] / 1e9
-        # scan kernels bracketed per call (k_entries; k_chunks + k_entries on the batch path)
-        scan_s_per_step = r["scan_ms"] / args.steps / 1e3
-        achieved = r["total"] / scan_s_per_step / 1e9 if scan_s_per_step > 0 else None
-        from oracle import oracle
-        ok = (bool(np.array_equal(r["crcs"], oracle.entries(r["host"], r["offs"], r["lens"])))
-              if rank == 0 else None)
-        line = {
-            "metric": "device-resident CRC32C GB/s over 1M mixed log entries (100B/1KiB/4KiB Zipf)",
-            "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic", "config": {"workload": f"{r['n']} entries, {r['total']} bytes per GPU",
-                                            "path": args.path,
-                                            "parallelism": f"replicas{world}" if world > 1 else "single",
-                                            "exchange": "none"},
-            "roofline": {"bound": "hbm", "kernel": "k_entries" if args.path == "entries" else "k_chunks+k_entries",
-                         "achieved": round(achieved, 1) if achieved else None,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                         "traffic": load_traffic("entries_scan") if args.path == "entries" else None,
-                         "scan_ms_per_step": round(scan_s_per_step * 1e3, 4)},
-            "bit_exact_vs_oracle": ok,
-        }
-    elif args.config == "replay":
-        from ramcloud_amd import segments
-        r = run_replay(args, ctx)
-        seg_total = r["nseg"] * r["seg_bytes"]
-        value = seg_total * args.steps / r["elapsed"] / 1e9
-        obj_bytes = int(r["counts"].sum()) * (segments.OBJECT_OVERHEAD + args.value_len - 4)
-        scan_s_per_step = r["scan_ms"] / args.steps / 1e3
-        achieved = obj_bytes / scan_s_per_step / 1e9 if scan_s_per_step > 0 else None
-        cpu = None if args.no_cpu_baseline else replay_cpu_baseline(
-            r["host"], r["seg_bytes"], r["certs"], min(args.replay_cpu_sample, r["nseg"]))
-        line = {
-            "metric": "device-resident recovery replay verify GB/s of 8 MiB object segments "
-                      "(segment walk + per-object checksum compare)",
-            "value": round(value, 2), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic (RecoverSegmentBenchmark-shaped objects, splitmix64 values)",
-            "config": {"workload": f"{r['nseg']} x {args.seg_mib} MiB segments of "
-                                   f"{args.value_len} B-value objects",
-                       "pipeline": (f"walk on {args.walk_cus} CUs beside the scan of the previous batch"
-                                    if args.walk_cus else "none"),
-                       "objects": int(r["counts"].sum()), "object_bytes_checksummed": obj_bytes},
-            "roofline": {"bound": "hbm", "kernel": "k_entries (object verify)",
-                         "achieved": round(achieved, 1) if achieved else None,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                         "traffic": None, "scan_ms_per_step": round(scan_s_per_step * 1e3, 4)},
-            "cpu_baseline": cpu,
-            "all_segments_verified": r["ok"],
-        }
-    elif args.config == "append":
-        line = run_append(args, ctx)
-    else:  # stream (config 5): host-to-host
-        seg_bytes = args.seg_mib * MiB
-        nseg = args.nseg
-        host = torch.empty(nseg * seg_bytes, dtype=torch.uint8).pin_memory()
-        dev = torch.empty(nseg * seg_bytes, dtype=torch.uint8, device="cuda")
-        workloads.splitmix_fill_segments(dev, seg_bytes, workloads.SEGMENT_SEED)
-        host.copy_(dev)
-        del dev
-        torch.cuda.synchronize()
-        out = ctx.stream_host(host, seg_bytes, nseg)
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            out = ctx.stream_host(host, seg_bytes, nseg, batch=8, depth=3)
-        elapsed = time.perf_counter() - t0
-        value = nseg * seg_bytes * args.steps / elapsed / 1e9
-        line = {"metric": "host-to-host streamed CRC32C GB/s (pinned H2D overlapped)",
-                "value": round(value, 2), "unit": "GB/s", "n_gpus": 1, "steps": args.steps,
-                "warmup": 1, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-                "data": "synthetic", "config": {"workload": f"{nseg} x {args.seg_mib} MiB pinned host segments"},
-                "first_crc": int(out[0])}
-
-    if rank == 0:
+        return 0
+    if args.host_dry_run:
+        ranks = Ranks("gloo")
+        line = run_recovery_host_dry(args, ranks)
+    else:
+        import torch
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        ranks = Ranks("nccl")
+        config = args.config
+        if config == "segments":
+            config = "c2" if ranks.world == 1 else "recovery"
+        run = {"c2": run_c2, "recovery": run_recovery, "entries": run_entries,
+               "replay": run_replay, "append": run_append, "stream": run_stream}[config]
+        line = run(args, ranks)
+    if ranks.rank == 0:
         print(json.dumps(line), flush=True)
-    ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
+    ranks.close()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

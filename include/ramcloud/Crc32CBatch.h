@@ -81,27 +81,45 @@ class Crc32CBatch {
         return out;
     }
 
-    /// Device-resident uniform segments (the recovery-scan shard): d_out[i]
-    /// for segment i = d_base + i * segmentBytes.  Asynchronous on `stream`.
+    /// Device-resident uniform segments (the recovery-scan batch): d_out[i]
+    /// for segment i = d_base + i * segmentBytes.  With wait (the default)
+    /// the call returns after the results are in d_out; wait = false leaves
+    /// it asynchronous on `stream`, to be followed by sync(stream).
     void
     deviceSegments(const void* d_base, uint64_t segmentBytes, uint64_t count,
-                   uint32_t* d_out, void* stream = NULL, bool finalize = true)
+                   uint32_t* d_out, void* stream = NULL, bool finalize = true, bool wait = true)
     {
         check(ramcrc_segments_device(context(), d_base, segmentBytes, count, NULL, d_out,
                                      finalize ? RAMCRC_FINALIZE : 0u, stream),
               "ramcrc_segments_device");
+        if (wait)
+            sync(stream);
     }
 
     /// Device-resident (offset, length) table, e.g. the (off + 4, len - 4)
-    /// object ranges of a recovery segment.  Asynchronous on `stream`.
+    /// object ranges of a recovery segment.  wait: as for deviceSegments.
+    /// A batch the context's scratch cannot plan (overlapping buffers
+    /// totalling more than the device holds) throws instead of leaving
+    /// d_out unwritten.
     void
     deviceBatch(const void* d_base, const uint64_t* d_off, const uint64_t* d_len,
                 const uint32_t* d_init, uint32_t* d_out, uint64_t count, void* stream = NULL,
-                bool finalize = true)
+                bool finalize = true, bool wait = true)
     {
         check(ramcrc_batch_device(context(), d_base, d_off, d_len, d_init, d_out, count,
                                   finalize ? RAMCRC_FINALIZE : 0u, stream),
               "ramcrc_batch_device");
+        if (wait)
+            sync(stream);
+    }
+
+    /// Waits for `stream` and throws if a launch of this object was refused
+    /// since the last sync (ramcrc_ctx_check): the outputs of a refused
+    /// launch are not written, and an integrity path must not read them.
+    void
+    sync(void* stream = NULL)
+    {
+        check(ramcrc_ctx_check(context(), stream), "ramcrc_ctx_check");
     }
 
     /**
@@ -111,8 +129,11 @@ class Crc32CBatch {
      * on the entries of the segments that passed (src/ObjectManager.cc:580-1100).
      * Segment i = d_base + i * stride, `capacity` bytes.  d_status[i] gets the
      * flags, metadata checksum, entry count and failed checks; d_entries /
-     * d_objCrc the walked records and their computed CRCs.  Asynchronous on
-     * `stream`; see ramcrc_segment_walk_device / ramcrc_verify_objects_device.
+     * d_objCrc the walked records and their computed CRCs.  Returns after
+     * both kernels finished on `stream` (see ramcrc_segment_walk_device /
+     * ramcrc_verify_objects_device).  A segment whose records did not fit
+     * in entriesCap carries RAMCRC_SEG_TABLE_FULL and never RAMCRC_SEG_OK:
+     * it was not verified; walk it again with a larger table.
      */
     void
     deviceReplayVerify(const void* d_base, uint64_t stride, uint32_t capacity, uint64_t count,
@@ -126,6 +147,7 @@ class Crc32CBatch {
         check(ramcrc_verify_objects_device(context(), d_base, stride, d_entries, entriesCap,
                                            d_nEntries, d_objCrc, d_status, stream),
               "ramcrc_verify_objects_device");
+        sync(stream);
     }
 
     /**
@@ -170,6 +192,96 @@ class Crc32CBatch {
 
     Crc32CBatch(const Crc32CBatch&);             // not copyable
     Crc32CBatch& operator=(const Crc32CBatch&);
+};
+
+/**
+ * The recovery-scan batch sharded across the GPUs of a node (ramcrc_shard_*,
+ * SURVEY.md 8(e)): every rank scans the contiguous range of replicas that
+ * sits in its own HBM and one RCCL all-gather of the 4-byte results leaves
+ * all CRCs, in segment order, with every rank -- what
+ * BackupMasterRecovery::CyclicReplicaBuffer::buildNext
+ * (src/BackupMasterRecovery.cc:743-809) checks per replica, for a whole
+ * batch at once.  Errors throw like Crc32CBatch's.
+ */
+class Crc32CShard {
+  public:
+    /// One process driving several GPUs (ncclCommInitAll).
+    explicit Crc32CShard(const std::vector<int>& devices)
+        : shard(NULL)
+    {
+        check(ramcrc_shard_create_all(devices.empty() ? NULL : &devices[0],
+                                      static_cast<int>(devices.size()), &shard),
+              "ramcrc_shard_create_all");
+    }
+
+    /// One process per GPU (ncclCommInitRank); every process passes the same
+    /// uniqueId() bytes, produced by one of them.
+    Crc32CShard(const std::vector<uint8_t>& id, int nranks, int rank, int device)
+        : shard(NULL)
+    {
+        if (id.size() != RAMCRC_SHARD_ID_BYTES)
+            RAMCRC_BATCH_THROW(std::string("Crc32CShard: unique id must be 128 bytes"));
+        check(ramcrc_shard_create_rank(&id[0], nranks, rank, device, &shard),
+              "ramcrc_shard_create_rank");
+    }
+
+    ~Crc32CShard()
+    {
+        if (shard)
+            ramcrc_shard_destroy(shard);
+    }
+
+    static std::vector<uint8_t>
+    uniqueId()
+    {
+        std::vector<uint8_t> id(RAMCRC_SHARD_ID_BYTES);
+        check(ramcrc_shard_unique_id(&id[0]), "ramcrc_shard_unique_id");
+        return id;
+    }
+
+    /// [first, last) of the segments rank `rank` of `nranks` owns.
+    static std::pair<uint64_t, uint64_t>
+    range(uint64_t segments, int nranks, int rank)
+    {
+        uint64_t lo = 0, hi = 0;
+        check(ramcrc_shard_range(segments, nranks, rank, &lo, &hi), "ramcrc_shard_range");
+        return std::make_pair(lo, hi);
+    }
+
+    /**
+     * One recovery-scan step: dShard[k] (device memory of local rank k)
+     * holds that rank's range() of `segments` replicas of segmentBytes each.
+     * Returns the finalized CRCs of all segments, in segment order, as
+     * gathered on local rank 0.  Synchronous.
+     */
+    std::vector<uint32_t>
+    deviceShard(const std::vector<const void*>& dShard, uint64_t segmentBytes,
+                uint64_t segments)
+    {
+        if (static_cast<int>(dShard.size()) != ramcrc_shard_local_count(shard))
+            RAMCRC_BATCH_THROW(std::string("Crc32CShard: one buffer per local rank"));
+        std::vector<uint32_t> out(segments);
+        check(ramcrc_shard_segments(shard, dShard.empty() ? NULL : &dShard[0], segmentBytes,
+                                    segments, NULL, RAMCRC_FINALIZE),
+              "ramcrc_shard_segments");
+        check(ramcrc_shard_sync(shard), "ramcrc_shard_sync");
+        if (segments)
+            check(ramcrc_shard_results(shard, 0, &out[0], segments), "ramcrc_shard_results");
+        return out;
+    }
+
+  private:
+    static void
+    check(int rc, const char* what)
+    {
+        if (rc != RAMCRC_OK)
+            RAMCRC_BATCH_THROW(std::string(what) + ": " + ramcrc_strerror(rc));
+    }
+
+    ramcrc_shard* shard;
+
+    Crc32CShard(const Crc32CShard&);             // not copyable
+    Crc32CShard& operator=(const Crc32CShard&);
 };
 
 } // namespace RAMCloud

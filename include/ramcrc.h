@@ -37,7 +37,9 @@ enum {
     RAMCRC_ENOMEM = -2,   /* device or pinned allocation failed */
     RAMCRC_EHIP = -3,     /* a HIP runtime call failed; see ramcrc_last_hip_error */
     RAMCRC_ENODEV = -4,   /* no usable gfx950 device */
-    RAMCRC_ERCCL = -5     /* RCCL failure (multi-GPU shard) */
+    RAMCRC_ERCCL = -5,    /* RCCL failure or RCCL unavailable (multi-GPU shard) */
+    RAMCRC_EREFUSED = -6  /* a launch found more chunks than the context's scratch holds and
+                             wrote none of its outputs (see ramcrc_ctx_check) */
 };
 
 /* Output flag: apply the final inversion (Crc32C::getResult, src/Crc32C.h:247).
@@ -158,7 +160,11 @@ typedef struct ramcrc_seg_status {
 #define RAMCRC_SEG_PAST_CAPACITY 2u   /* an entry ran past the segment capacity (src/Segment.cc:777-783) */
 #define RAMCRC_SEG_PAST_LENGTH 4u     /* entries ran past certificate.segmentLength (:786-790) */
 #define RAMCRC_SEG_BAD_CHECKSUM 8u    /* certificate checksum mismatch (:795-797) */
-#define RAMCRC_SEG_TABLE_FULL 16u     /* entry table capacity exhausted: records dropped */
+#define RAMCRC_SEG_TABLE_FULL 16u     /* entry table capacity exhausted: records of this segment
+                                         were dropped, so it is NOT verified -- RAMCRC_SEG_OK is
+                                         never set with this flag and none of its records are
+                                         checked; size entries_cap for the smallest entry the
+                                         segments can hold and walk again */
 #define RAMCRC_SEG_CYCLE 32u          /* the walk revisited an offset (uint32_t wrap): the
                                          reference's loop would not terminate; stopped */
 #define RAMCRC_LOG_ENTRY_TYPE_OBJ 2u          /* LOG_ENTRY_TYPE_OBJ, src/LogEntryTypes.h:35 */
@@ -237,6 +243,79 @@ int ramcrc_verify_objects_device(ramcrc_ctx* ctx, const void* d_base, uint64_t s
 int ramcrc_segment_fill_objects(uint8_t* seg, uint32_t capacity, uint32_t value_len,
                                 uint64_t first_key, uint32_t* n_objects, ramcrc_seg_cert* cert);
 
+/* Device form of ramcrc_segment_fill_objects for n_seg segments at d_base +
+ * i*seg_stride (RecoverSegmentBenchmark::run's input, the BASELINE C4 shard,
+ * built where it is scanned): segment i holds keys first_key + i*per ..
+ * first_key + (i+1)*per - 1, per = objects per segment; value bytes are
+ * whatever the segments already hold; bytes after the last entry are zeroed;
+ * every Object::Header::checksum is computed by the batch kernels.  The
+ * layout equals ramcrc_segment_fill_objects' byte for byte.  Every segment
+ * gets the same certificate (the metadata checksum covers only entry headers
+ * and lengths): written to *h_cert, to d_certs[i] when d_certs (device) is
+ * not NULL, and per to *h_objects.  seg_stride >= capacity.  Synchronous. */
+int ramcrc_segment_fill_objects_device(ramcrc_ctx* ctx, void* d_base, uint64_t seg_stride,
+                                       uint32_t capacity, uint64_t n_seg, uint32_t value_len,
+                                       uint64_t first_key, ramcrc_seg_cert* d_certs,
+                                       ramcrc_seg_cert* h_cert, uint32_t* h_objects);
+
+/* ------------------------------------------- multi-GPU recovery shard --- */
+
+/* The recovery-scan batch sharded across GPUs: a backup's
+ * replicas are verified independently (BackupMasterRecovery::
+ * CyclicReplicaBuffer::buildNext, src/BackupMasterRecovery.cc:743-809), so
+ * rank r of N scans the contiguous segment range ramcrc_shard_range(nseg, N,
+ * r) held in its own GPU's HBM, and one RCCL all-gather of the 4-byte
+ * results (the only exchange) leaves every rank with all CRCs in segment
+ * order.  Segment bytes never cross xGMI.  RCCL (librccl.so.1) is loaded
+ * at the first shard call; without it the shard calls return RAMCRC_ERCCL.
+ *
+ * Two ways to build one:
+ *   ramcrc_shard_create_all  one process drives `ndev` GPUs (ncclCommInitAll);
+ *                            local rank k = devices[k] = global rank k;
+ *   ramcrc_shard_create_rank one process per GPU (ncclCommInitRank): every
+ *                            process passes the same unique id (made by one
+ *                            of them with ramcrc_shard_unique_id and sent to
+ *                            the others out of band) and its own rank.
+ * A shard owns one stream and one ramcrc_ctx per local rank. */
+typedef struct ramcrc_shard ramcrc_shard;
+#define RAMCRC_SHARD_ID_BYTES 128
+
+int ramcrc_shard_unique_id(void* id /* RAMCRC_SHARD_ID_BYTES */);
+int ramcrc_shard_create_all(const int* devices, int ndev, ramcrc_shard** out);
+int ramcrc_shard_create_rank(const void* id, int nranks, int rank, int device,
+                             ramcrc_shard** out);
+int ramcrc_shard_destroy(ramcrc_shard* shard);
+
+/* Contiguous [lo, hi) of segment indices owned by `rank` (sizes differ by at
+ * most one; lower ranks get the extra ones).  Pure host arithmetic. */
+int ramcrc_shard_range(uint64_t nseg, int nranks, int rank, uint64_t* lo, uint64_t* hi);
+
+/* Local ranks this handle drives, and the global rank / device / stream /
+ * context of local rank k (for callers that order their own work against
+ * the shard, or time it with ramcrc_ctx_set_timing). */
+int ramcrc_shard_local_count(const ramcrc_shard* shard);
+int ramcrc_shard_info(const ramcrc_shard* shard, int k, int* rank, int* device, void** stream,
+                      ramcrc_ctx** ctx);
+
+/* One recovery-scan step.  For every local rank k (global rank r):
+ * d_shard[k] (on that rank's device) holds segments [lo_r, hi_r) of the
+ * batch at seg_bytes stride; after the step, d_all[k] (device, nseg uint32)
+ * holds the CRCs of all nseg segments in segment order -- or, when d_all is
+ * NULL, the shard's own result buffers do (ramcrc_shard_results).  flags:
+ * RAMCRC_FINALIZE as for ramcrc_segments_device.  Asynchronous on the
+ * shard's streams; a single-process shard issues the ranks' collectives in
+ * one RCCL group. */
+int ramcrc_shard_segments(ramcrc_shard* shard, const void* const* d_shard, uint64_t seg_bytes,
+                          uint64_t nseg, uint32_t* const* d_all, uint32_t flags);
+
+/* Wait for every local rank's stream; RAMCRC_ERCCL if RCCL reported an
+ * asynchronous error. */
+int ramcrc_shard_sync(ramcrc_shard* shard);
+
+/* Copy local rank k's gathered CRCs of the last step (when it ran with d_all
+ * == NULL) to host memory; synchronous. */
+int ramcrc_shard_results(ramcrc_shard* shard, int k, uint32_t* h_out, uint64_t nseg);
+
 /* ------------------------------------------------- batched write path --- */
 
 /* Object::assembleForLog's checksum (src/Object.cc:213-238; the value is
@@ -283,9 +362,19 @@ int ramcrc_stream_create_cu_mask(int device, const uint32_t* cu_mask, uint32_t m
 int ramcrc_stream_destroy(void* stream);
 int ramcrc_ctx_set_cus(ramcrc_ctx* ctx, int ncu);
 
-/* Nonzero if a planned launch found more chunks than the context's scratch
- * holds (its outputs were not written); raise ramcrc_ctx_reserve.  Synchronous. */
+/* Raw launch status word of the context (bit 0: the latest planned launch
+ * found more chunks than the scratch holds and wrote none of its outputs;
+ * bit 1: some launch did since the last ramcrc_ctx_check).  Synchronous. */
 int ramcrc_ctx_status(ramcrc_ctx* ctx, uint32_t* status);
+
+/* Waits for `stream`, then returns RAMCRC_EREFUSED (and clears the sticky
+ * bit) if any launch of this context was refused since the last check,
+ * RAMCRC_OK otherwise.  A refusal needs a general batch whose buffers
+ * overlap or total more bytes than the device holds (ramcrc_batch_device,
+ * ramcrc_verify_objects_device, ramcrc_assemble_objects_device); raise
+ * ramcrc_ctx_reserve and retry.  The host entry points (ramcrc_batch_host,
+ * ramcrc_assemble_objects_host) check by themselves. */
+int ramcrc_ctx_check(ramcrc_ctx* ctx, void* stream);
 
 /* Diagnostics. */
 const char* ramcrc_strerror(int code);

@@ -399,7 +399,7 @@ uint32_t oracle_check_metadata(const uint8_t* seg, uint64_t capacity, uint32_t c
             flags |= fin == cert_crc ? 1 : 8;
     }
     if (table && n > table_cap)
-        flags |= 16;
+        flags = (flags | 16) & ~1u;   /* records dropped: the segment is not verified */
     if (checksum_out)
         *checksum_out = fin;
     if (n_out)

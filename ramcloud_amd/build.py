@@ -18,7 +18,7 @@ LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libramcrc.so")
 ARCH = "gfx950"
 
-SOURCES = ["ramcrc_device.hip", "ramcrc_host.cc"]
+SOURCES = ["ramcrc_device.hip", "ramcrc_host.cc", "ramcrc_shard.hip", "ramcrc_fill.hip"]
 HEADERS = ["gf2.h"]
 
 
@@ -47,7 +47,7 @@ def _compile(out, defines=(), verbose=False):
            "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
     cmd += ["-D" + d for d in defines]
     cmd += [os.path.join(CSRC, s) for s in SOURCES]
-    cmd += ["-o", tmp]
+    cmd += ["-ldl", "-o", tmp]
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)

@@ -426,7 +426,7 @@ struct Plan {
     uint64_t ngroups;
     uint32_t* partials;
     uint64_t partials_cap;
-    uint32_t* status;      // bit 0: partials overflow
+    uint32_t* status;      // bit 0: this launch's partials overflow; bit 1: sticky (ramcrc_ctx_check)
     unsigned long long* ticket;   // chunk dequeue counter; zero between launches
 };
 
@@ -586,7 +586,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_chunks(BatchDesc d, Plan pl, ui
     const uint64_t total = kMode == kSegAligned ? per_seg * d.n : pl.group_pref[pl.ngroups];
     if (total > pl.partials_cap) {
         if (wave == 0 && lane == 0)
-            atomicOr(pl.status, 1u);
+            atomicOr(pl.status, 3u);   // refused: this launch, and sticky until checked
         return;
     }
     // Work: chunk g -> (buffer i, chunk k).  Dynamic: lane 0 takes tickets
@@ -1495,7 +1495,7 @@ __global__ __launch_bounds__(kThreads) void k_plan_scan(Plan pl)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     if (threadIdx.x == 0) {
         carry_s = 0;
-        *pl.status = 0;   // stream-ordered before this launch's k_chunks
+        *pl.status &= ~1u;   // stream-ordered before this launch's k_chunks (bit 1 stays)
         *pl.ticket = 0;
     }
     __syncthreads();
@@ -1560,7 +1560,7 @@ struct ramcrc_ctx {
     int device = 0;
     int ncu = 256;       // CUs the persistent grids are sized for (ramcrc_ctx_set_cus)
     int ncu_all = 256;   // CUs of the device
-    std::mutex mu;
+    std::recursive_mutex mu;   // recursive: the host entry points hold it across their inner device calls
     uint32_t* partials = nullptr;
     uint64_t partials_cap = 0;
     uint64_t* plan_local = nullptr;
@@ -1994,10 +1994,10 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
         if (!(flags & (RAMCRC_SEG_PAST_CAPACITY | RAMCRC_SEG_CYCLE))) {
             if (pos > cert.segment_length)
                 flags |= RAMCRC_SEG_PAST_LENGTH;
-            else if (fin == cert.checksum)
-                flags |= RAMCRC_SEG_OK;
-            else
+            else if (fin != cert.checksum)
                 flags |= RAMCRC_SEG_BAD_CHECKSUM;
+            else if (!(flags & RAMCRC_SEG_TABLE_FULL))
+                flags |= RAMCRC_SEG_OK;   // records dropped: not verified, never OK
         }
         if (lane == 0) {
             ramcrc_seg_status st;
@@ -2172,6 +2172,7 @@ const char* ramcrc_strerror(int code)
     case RAMCRC_EHIP: return hipGetErrorString(hipError_t(t_last_hip));
     case RAMCRC_ENODEV: return "no usable device";
     case RAMCRC_ERCCL: return "rccl failure";
+    case RAMCRC_EREFUSED: return "launch refused: chunk scratch too small (ramcrc_ctx_reserve)";
     default: return "unknown error";
     }
 }
@@ -2255,7 +2256,7 @@ int ramcrc_ctx_reserve(ramcrc_ctx* c, uint64_t max_chunks, uint64_t max_entries)
 {
     if (!c)
         return RAMCRC_EINVAL;
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceGuard g(c->device);
     return reserve_locked(c, max_chunks, max_entries);
 }
@@ -2264,7 +2265,7 @@ int ramcrc_ctx_set_timing(ramcrc_ctx* c, int enable)
 {
     if (!c)
         return RAMCRC_EINVAL;
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     c->timing = enable != 0;
     return RAMCRC_OK;
 }
@@ -2295,7 +2296,7 @@ int ramcrc_ctx_set_cus(ramcrc_ctx* c, int ncu)
 {
     if (!c || ncu < 0)
         return RAMCRC_EINVAL;
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     if (ncu == 0 || ncu > c->ncu_all)
         ncu = c->ncu_all;
     c->ncu = ncu;
@@ -2306,7 +2307,7 @@ int ramcrc_ctx_scan_time(ramcrc_ctx* c, double* total_ms, uint64_t* launches)
 {
     if (!c)
         return RAMCRC_EINVAL;
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceGuard g(c->device);
     double sum = 0;
     uint64_t cnt = 0;
@@ -2335,6 +2336,22 @@ int ramcrc_ctx_status(ramcrc_ctx* c, uint32_t* status)
     return RAMCRC_OK;
 }
 
+int ramcrc_ctx_check(ramcrc_ctx* c, void* stream)
+{
+    if (!c)
+        return RAMCRC_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    HIPCHK(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+    uint32_t st = 0;
+    HIPCHK(hipMemcpy(&st, c->status, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (!(st & 2u))
+        return RAMCRC_OK;
+    const uint32_t cleared = st & ~3u;
+    HIPCHK(hipMemcpy(c->status, &cleared, sizeof(uint32_t), hipMemcpyHostToDevice));
+    return RAMCRC_EREFUSED;
+}
+
 int ramcrc_segments_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_bytes, uint64_t nseg,
                            const uint32_t* d_init, uint32_t* d_out, uint32_t flags, void* stream)
 {
@@ -2342,7 +2359,7 @@ int ramcrc_segments_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_bytes
         return RAMCRC_EINVAL;
     if (nseg == 0)
         return RAMCRC_OK;
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceGuard g(c->device);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     BatchDesc d{};
@@ -2397,7 +2414,7 @@ int ramcrc_batch_device(ramcrc_ctx* c, const void* d_base, const uint64_t* d_off
         return c ? RAMCRC_OK : RAMCRC_EINVAL;
     if (!c || !d_out || !d_off || !d_len || !d_base)
         return RAMCRC_EINVAL;
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceGuard g(c->device);
     int rc = reserve_locked(c, default_chunk_bound(n), n);
     if (rc)
@@ -2422,7 +2439,7 @@ int ramcrc_entries_device(ramcrc_ctx* c, const void* d_base, const uint64_t* d_o
         return c ? RAMCRC_OK : RAMCRC_EINVAL;
     if (!c || !d_out || !d_off || !d_len || !d_base)
         return RAMCRC_EINVAL;
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceGuard g(c->device);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     BatchDesc d{};
@@ -2444,36 +2461,40 @@ int ramcrc_batch_host(ramcrc_ctx* c, const void* const* ptrs, const uint64_t* le
         return RAMCRC_EINVAL;
     if (n == 0)
         return RAMCRC_OK;
+    // The context lock is held from sizing the staging buffers to the final
+    // synchronize: another thread on this context must not free or refill
+    // them while they are being copied from.
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceGuard g(c->device);
     // Pack every buffer 16-byte aligned into one pinned staging area, then one
     // H2D copy, one batch launch, one D2H copy.
     uint64_t total = 0;
-    for (uint64_t i = 0; i < n; i++)
+    for (uint64_t i = 0; i < n; i++) {
+        if (lens[i] && !ptrs[i])
+            return RAMCRC_EINVAL;
         total += (lens[i] + 15) & ~uint64_t(15);
+    }
     const uint64_t meta = n * (2 * sizeof(uint64_t) + 2 * sizeof(uint32_t));
     const uint64_t need = total + meta + 64;
-    {
-        std::lock_guard<std::mutex> lk(c->mu);
-        if (c->h_stage_cap < need) {
-            if (c->h_stage) (void)hipHostFree(c->h_stage);
-            c->h_stage = nullptr;
-            c->h_stage_cap = 0;
-            if (hipHostMalloc(reinterpret_cast<void**>(&c->h_stage), need, hipHostMallocDefault) !=
-                hipSuccess)
-                return RAMCRC_ENOMEM;
-            c->h_stage_cap = need;
-        }
-        if (c->d_stage_cap < need) {
-            if (c->d_stage) (void)hipFree(c->d_stage);
-            c->d_stage = nullptr;
-            c->d_stage_cap = 0;
-            if (hipMalloc(reinterpret_cast<void**>(&c->d_stage), need) != hipSuccess)
-                return RAMCRC_ENOMEM;
-            c->d_stage_cap = need;
-        }
-        if (!c->copy_stream)
-            HIPCHK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    if (c->h_stage_cap < need) {
+        if (c->h_stage) (void)hipHostFree(c->h_stage);
+        c->h_stage = nullptr;
+        c->h_stage_cap = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&c->h_stage), need, hipHostMallocDefault) !=
+            hipSuccess)
+            return RAMCRC_ENOMEM;
+        c->h_stage_cap = need;
     }
+    if (c->d_stage_cap < need) {
+        if (c->d_stage) (void)hipFree(c->d_stage);
+        c->d_stage = nullptr;
+        c->d_stage_cap = 0;
+        if (hipMalloc(reinterpret_cast<void**>(&c->d_stage), need) != hipSuccess)
+            return RAMCRC_ENOMEM;
+        c->d_stage_cap = need;
+    }
+    if (!c->copy_stream)
+        HIPCHK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
     uint8_t* h = c->h_stage;
     uint64_t* h_off = reinterpret_cast<uint64_t*>(h + total);
     uint64_t* h_len = h_off + n;
@@ -2497,10 +2518,14 @@ int ramcrc_batch_host(ramcrc_ctx* c, const void* const* ptrs, const uint64_t* le
     uint32_t* d_init = reinterpret_cast<uint32_t*>(d_len + n);
     uint32_t* d_out = d_init + n;
     int rc = ramcrc_batch_device(c, d, d_off, d_len, d_init, d_out, n, flags, s);
+    if (rc) {
+        (void)hipStreamSynchronize(s);   // the H2D copy reads h_stage
+        return rc;
+    }
+    HIPCHK(hipMemcpyAsync(h_out, d_out, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    rc = ramcrc_ctx_check(c, s);   // synchronizes s; a refused launch wrote nothing
     if (rc)
         return rc;
-    HIPCHK(hipMemcpyAsync(h_out, d_out, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
     memcpy(out, h_out, n * sizeof(uint32_t));
     return RAMCRC_OK;
 }
@@ -2512,6 +2537,7 @@ int ramcrc_stream_host(ramcrc_ctx* c, const void* h_base, uint64_t seg_bytes, ui
         return RAMCRC_EINVAL;
     if (nseg == 0)
         return RAMCRC_OK;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);   // held until both streams drained
     DeviceGuard g(c->device);
     if (depth > 8)
         depth = 8;
@@ -2519,54 +2545,63 @@ int ramcrc_stream_host(ramcrc_ctx* c, const void* h_base, uint64_t seg_bytes, ui
     // Each slot: batch*seg_bytes of data + batch CRCs.
     const uint64_t slot_stride = (slot_bytes + 4 * uint64_t(batch) + 4095) & ~uint64_t(4095);
     const uint64_t need = slot_stride * uint64_t(depth);
-    {
-        std::lock_guard<std::mutex> lk(c->mu);
-        if (c->d_stage_cap < need) {
-            if (c->d_stage) (void)hipFree(c->d_stage);
-            c->d_stage = nullptr;
-            c->d_stage_cap = 0;
-            if (hipMalloc(reinterpret_cast<void**>(&c->d_stage), need) != hipSuccess)
-                return RAMCRC_ENOMEM;
-            c->d_stage_cap = need;
-        }
-        if (!c->copy_stream)
-            HIPCHK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
-        if (!c->compute_stream)
-            HIPCHK(hipStreamCreateWithFlags(&c->compute_stream, hipStreamNonBlocking));
+    if (c->d_stage_cap < need) {
+        if (c->d_stage) (void)hipFree(c->d_stage);
+        c->d_stage = nullptr;
+        c->d_stage_cap = 0;
+        if (hipMalloc(reinterpret_cast<void**>(&c->d_stage), need) != hipSuccess)
+            return RAMCRC_ENOMEM;
+        c->d_stage_cap = need;
     }
-    hipEvent_t copied[8], done[8];
-    for (int k = 0; k < depth; k++) {
-        HIPCHK(hipEventCreateWithFlags(&copied[k], hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&done[k], hipEventDisableTiming));
+    if (!c->copy_stream)
+        HIPCHK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    if (!c->compute_stream)
+        HIPCHK(hipStreamCreateWithFlags(&c->compute_stream, hipStreamNonBlocking));
+    hipEvent_t copied[8] = {}, done[8] = {};
+    int rc = RAMCRC_OK;
+    auto hip = [&](hipError_t e) {
+        if (e != hipSuccess && rc == RAMCRC_OK) {
+            t_last_hip = int(e);
+            rc = RAMCRC_EHIP;
+        }
+        return rc == RAMCRC_OK;
+    };
+    for (int k = 0; k < depth && rc == RAMCRC_OK; k++) {
+        hip(hipEventCreateWithFlags(&copied[k], hipEventDisableTiming));
+        hip(hipEventCreateWithFlags(&done[k], hipEventDisableTiming));
     }
     const uint8_t* src = static_cast<const uint8_t*>(h_base);
-    int rc = RAMCRC_OK;
-    uint64_t nb = (nseg + batch - 1) / batch;
+    const uint64_t nb = (nseg + batch - 1) / batch;
+    // On any failure the loop stops issuing; the streams are drained below
+    // before the events are destroyed and before returning, so no copy into
+    // h_out or out of h_base is still in flight when the call returns.
     for (uint64_t b = 0; b < nb && rc == RAMCRC_OK; b++) {
         const int k = int(b % depth);
         const uint64_t first = b * batch;
         const uint64_t cnt = (nseg - first) < uint64_t(batch) ? (nseg - first) : uint64_t(batch);
         uint8_t* slot = c->d_stage + uint64_t(k) * slot_stride;
         uint32_t* slot_out = reinterpret_cast<uint32_t*>(slot + slot_bytes);
-        if (b >= uint64_t(depth))
-            HIPCHK(hipStreamWaitEvent(c->copy_stream, done[k], 0));
-        HIPCHK(hipMemcpyAsync(slot, src + first * seg_bytes, cnt * seg_bytes,
-                              hipMemcpyHostToDevice, c->copy_stream));
-        HIPCHK(hipEventRecord(copied[k], c->copy_stream));
-        HIPCHK(hipStreamWaitEvent(c->compute_stream, copied[k], 0));
+        if (b >= uint64_t(depth) && !hip(hipStreamWaitEvent(c->copy_stream, done[k], 0)))
+            break;
+        if (!hip(hipMemcpyAsync(slot, src + first * seg_bytes, cnt * seg_bytes,
+                                hipMemcpyHostToDevice, c->copy_stream)) ||
+            !hip(hipEventRecord(copied[k], c->copy_stream)) ||
+            !hip(hipStreamWaitEvent(c->compute_stream, copied[k], 0)))
+            break;
         rc = ramcrc_segments_device(c, slot, seg_bytes, cnt, nullptr, slot_out, flags,
                                     c->compute_stream);
         if (rc)
             break;
-        HIPCHK(hipMemcpyAsync(h_out + first, slot_out, cnt * sizeof(uint32_t),
-                              hipMemcpyDeviceToHost, c->compute_stream));
-        HIPCHK(hipEventRecord(done[k], c->compute_stream));
+        if (!hip(hipMemcpyAsync(h_out + first, slot_out, cnt * sizeof(uint32_t),
+                                hipMemcpyDeviceToHost, c->compute_stream)) ||
+            !hip(hipEventRecord(done[k], c->compute_stream)))
+            break;
     }
-    HIPCHK(hipStreamSynchronize(c->compute_stream));
-    HIPCHK(hipStreamSynchronize(c->copy_stream));
+    hip(hipStreamSynchronize(c->compute_stream));
+    hip(hipStreamSynchronize(c->copy_stream));
     for (int k = 0; k < depth; k++) {
-        (void)hipEventDestroy(copied[k]);
-        (void)hipEventDestroy(done[k]);
+        if (copied[k]) (void)hipEventDestroy(copied[k]);
+        if (done[k]) (void)hipEventDestroy(done[k]);
     }
     return rc;
 }
@@ -2585,7 +2620,7 @@ int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_s
     if ((reinterpret_cast<uintptr_t>(d_base) & 15) || (seg_stride & 15) || (seg_capacity & 15) ||
         n_seg > 0xFFFFFFFFull || (n_seg > 1 && seg_stride < seg_capacity))
         return RAMCRC_EINVAL;
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceGuard g(c->device);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     HIPCHK(hipMemsetAsync(d_n_entries, 0, sizeof(uint64_t), s));
@@ -2620,7 +2655,7 @@ int ramcrc_verify_objects_device(ramcrc_ctx* c, const void* d_base, uint64_t seg
         return RAMCRC_OK;
     if (!d_base || !d_entries || !d_n_entries || !d_obj_crc || !d_status)
         return RAMCRC_EINVAL;
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceGuard g(c->device);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int rc = reserve_locked(c, default_chunk_bound(entries_cap), entries_cap);
@@ -2653,7 +2688,7 @@ int ramcrc_assemble_objects_device(ramcrc_ctx* c, void* d_base, const uint64_t* 
         return c ? RAMCRC_OK : RAMCRC_EINVAL;
     if (!c || !d_base || !d_off || !d_len)
         return RAMCRC_EINVAL;
-    std::lock_guard<std::mutex> lk(c->mu);
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceGuard g(c->device);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int rc = reserve_locked(c, default_chunk_bound(n), n);

@@ -1,0 +1,452 @@
+// Multi-GPU recovery-scan shard (include/ramcrc.h, "multi-GPU recovery
+// shard"): the C-ABI a RAMCloud backup process (C++, no torch) calls to
+// spread one recovery batch of replicas over the GPUs of a node.
+//
+// Reference behaviour: BackupMasterRecovery::CyclicReplicaBuffer::buildNext
+// (src/BackupMasterRecovery.cc:743-809) verifies every loaded 8 MiB replica
+// on its own -- no replica needs another's bytes -- so the batch partitions
+// into contiguous segment ranges, one per GPU, with no data exchange.  The
+// only collective is one RCCL all-gather of the 4-byte per-segment results
+// (1 KiB per rank at 256 segments per GPU), after which every rank holds the
+// whole batch's CRCs in segment order for host-side comparison.
+//
+// Layout of one step on rank r of N (nseg segments, width = ceil(nseg / N)):
+//   gather[r * width + j] = CRC of segment lo_r + j      (ramcrc_segments_device)
+//   ncclAllGather in place: gather[q * width + j] on every rank
+//   all[s] = gather[q(s) * width + (s - lo_q)]            (k_unpad; skipped
+//                                                         when N divides nseg
+//                                                         and all == gather)
+// RCCL is resolved with dlopen at the first shard call: torch (when present)
+// has already loaded librccl.so.1 under the same soname, so one RCCL serves
+// the process either way, and programs that never shard need no RCCL at all.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <dlfcn.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "ramcrc.h"
+
+namespace {
+
+struct Rccl {
+    ncclResult_t (*get_unique_id)(ncclUniqueId*);
+    ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*);
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int);
+    ncclResult_t (*comm_destroy)(ncclComm_t);
+    ncclResult_t (*comm_async_error)(ncclComm_t, ncclResult_t*);
+    ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t,
+                               hipStream_t);
+    ncclResult_t (*group_start)();
+    ncclResult_t (*group_end)();
+    const char* (*error_string)(ncclResult_t);
+};
+
+const Rccl* rccl()
+{
+    static Rccl r;
+    static bool ok = false;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h)
+            h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            fprintf(stderr, "ramcrc: RCCL not loadable: %s\n", dlerror());
+            return;
+        }
+        bool all = true;
+        auto sym = [&](const char* name) {
+            void* p = dlsym(h, name);
+            all = all && p;
+            return p;
+        };
+        r.get_unique_id = reinterpret_cast<decltype(r.get_unique_id)>(sym("ncclGetUniqueId"));
+        r.comm_init_all = reinterpret_cast<decltype(r.comm_init_all)>(sym("ncclCommInitAll"));
+        r.comm_init_rank = reinterpret_cast<decltype(r.comm_init_rank)>(sym("ncclCommInitRank"));
+        r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(sym("ncclCommDestroy"));
+        r.comm_async_error =
+            reinterpret_cast<decltype(r.comm_async_error)>(sym("ncclCommGetAsyncError"));
+        r.all_gather = reinterpret_cast<decltype(r.all_gather)>(sym("ncclAllGather"));
+        r.group_start = reinterpret_cast<decltype(r.group_start)>(sym("ncclGroupStart"));
+        r.group_end = reinterpret_cast<decltype(r.group_end)>(sym("ncclGroupEnd"));
+        r.error_string = reinterpret_cast<decltype(r.error_string)>(sym("ncclGetErrorString"));
+        ok = all;
+        if (!ok)
+            fprintf(stderr, "ramcrc: librccl.so.1 lacks a required symbol\n");
+    });
+    return ok ? &r : nullptr;
+}
+
+int rccl_fail(const Rccl* r, ncclResult_t e, const char* what)
+{
+    fprintf(stderr, "ramcrc: %s: %s\n", what, r ? r->error_string(e) : "rccl unavailable");
+    return RAMCRC_ERCCL;
+}
+
+#define RCCLCHK(r, expr, what)                    \
+    do {                                          \
+        ncclResult_t e_ = (expr);                 \
+        if (e_ != ncclSuccess)                    \
+            return rccl_fail((r), e_, (what));    \
+    } while (0)
+
+#define HIPCHK_S(expr)                            \
+    do {                                          \
+        if ((expr) != hipSuccess)                 \
+            return RAMCRC_EHIP;                   \
+    } while (0)
+
+// all[s] = gather[q * width + s - lo_q] for the owner q of segment s.
+__global__ __launch_bounds__(256) void k_unpad(const uint32_t* gather, uint32_t* all, uint64_t nseg,
+                                               uint64_t width, uint64_t base, uint64_t rem)
+{
+    const uint64_t s = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (s >= nseg)
+        return;
+    // owners 0 .. rem-1 hold base + 1 segments, the others base
+    const uint64_t big = rem * (base + 1);
+    const uint64_t q = s < big ? s / (base + 1) : rem + (s - big) / base;
+    const uint64_t lo = q < rem ? q * (base + 1) : big + (q - rem) * base;
+    all[s] = gather[q * width + (s - lo)];
+}
+
+struct Local {
+    int rank = 0;
+    int device = 0;
+    ncclComm_t comm = nullptr;
+    hipStream_t stream = nullptr;
+    ramcrc_ctx* ctx = nullptr;
+    uint32_t* gather = nullptr;   // width * nranks
+    uint64_t gather_cap = 0;
+    uint32_t* all = nullptr;      // nseg (results when the caller passes no d_all)
+    uint64_t all_cap = 0;
+    uint64_t last_nseg = 0;
+    bool last_internal = false;
+};
+
+struct DevGuard {
+    int prev = -1;
+    explicit DevGuard(int d)
+    {
+        if (hipGetDevice(&prev) != hipSuccess)
+            prev = -1;
+        (void)hipSetDevice(d);
+    }
+    ~DevGuard()
+    {
+        if (prev >= 0)
+            (void)hipSetDevice(prev);
+    }
+};
+
+int grow(uint32_t** p, uint64_t* cap, uint64_t n)
+{
+    if (*cap >= n && *p)
+        return RAMCRC_OK;
+    if (*p) {
+        HIPCHK_S(hipDeviceSynchronize());
+        HIPCHK_S(hipFree(*p));
+        *p = nullptr;
+        *cap = 0;
+    }
+    const uint64_t want = n < 256 ? 256 : n;
+    if (hipMalloc(reinterpret_cast<void**>(p), want * sizeof(uint32_t)) != hipSuccess) {
+        *p = nullptr;
+        return RAMCRC_ENOMEM;
+    }
+    *cap = want;
+    return RAMCRC_OK;
+}
+
+}  // namespace
+
+struct ramcrc_shard {
+    int nranks = 0;
+    std::vector<Local> local;
+    std::mutex mu;
+};
+
+namespace {
+
+// Streams and contexts for every local rank (communicators already set).
+int finish_create(ramcrc_shard* sh)
+{
+    for (Local& l : sh->local) {
+        DevGuard g(l.device);
+        HIPCHK_S(hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking));
+        int rc = ramcrc_ctx_create(l.device, &l.ctx);
+        if (rc)
+            return rc;
+    }
+    return RAMCRC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ramcrc_shard_range(uint64_t nseg, int nranks, int rank, uint64_t* lo, uint64_t* hi)
+{
+    if (nranks < 1 || rank < 0 || rank >= nranks || !lo || !hi)
+        return RAMCRC_EINVAL;
+    const uint64_t base = nseg / uint64_t(nranks), rem = nseg % uint64_t(nranks);
+    const uint64_t r = uint64_t(rank);
+    *lo = r * base + (r < rem ? r : rem);
+    *hi = *lo + base + (r < rem ? 1 : 0);
+    return RAMCRC_OK;
+}
+
+int ramcrc_shard_unique_id(void* id)
+{
+    if (!id)
+        return RAMCRC_EINVAL;
+    const Rccl* r = rccl();
+    if (!r)
+        return RAMCRC_ERCCL;
+    ncclUniqueId u;
+    RCCLCHK(r, r->get_unique_id(&u), "ncclGetUniqueId");
+    static_assert(sizeof(u) == RAMCRC_SHARD_ID_BYTES, "ncclUniqueId size");
+    memcpy(id, &u, sizeof(u));
+    return RAMCRC_OK;
+}
+
+int ramcrc_shard_create_all(const int* devices, int ndev, ramcrc_shard** out)
+{
+    if (!out)
+        return RAMCRC_EINVAL;
+    *out = nullptr;
+    if (!devices || ndev < 1)
+        return RAMCRC_EINVAL;
+    int navail = 0;
+    if (hipGetDeviceCount(&navail) != hipSuccess)
+        return RAMCRC_ENODEV;
+    for (int k = 0; k < ndev; k++) {
+        if (devices[k] < 0 || devices[k] >= navail)
+            return RAMCRC_ENODEV;
+        for (int j = 0; j < k; j++)
+            if (devices[j] == devices[k])
+                return RAMCRC_EINVAL;   // one rank per GPU
+    }
+    const Rccl* r = rccl();
+    if (!r)
+        return RAMCRC_ERCCL;
+    ramcrc_shard* sh = new (std::nothrow) ramcrc_shard();
+    if (!sh)
+        return RAMCRC_ENOMEM;
+    sh->nranks = ndev;
+    sh->local.resize(ndev);
+    std::vector<ncclComm_t> comms(ndev, nullptr);
+    ncclResult_t e = r->comm_init_all(comms.data(), ndev, devices);
+    if (e != ncclSuccess) {
+        delete sh;
+        return rccl_fail(r, e, "ncclCommInitAll");
+    }
+    for (int k = 0; k < ndev; k++) {
+        sh->local[k].rank = k;
+        sh->local[k].device = devices[k];
+        sh->local[k].comm = comms[k];
+    }
+    int rc = finish_create(sh);
+    if (rc) {
+        ramcrc_shard_destroy(sh);
+        return rc;
+    }
+    *out = sh;
+    return RAMCRC_OK;
+}
+
+int ramcrc_shard_create_rank(const void* id, int nranks, int rank, int device, ramcrc_shard** out)
+{
+    if (!out)
+        return RAMCRC_EINVAL;
+    *out = nullptr;
+    if (!id || nranks < 1 || rank < 0 || rank >= nranks)
+        return RAMCRC_EINVAL;
+    int navail = 0;
+    if (hipGetDeviceCount(&navail) != hipSuccess || device < 0 || device >= navail)
+        return RAMCRC_ENODEV;
+    const Rccl* r = rccl();
+    if (!r)
+        return RAMCRC_ERCCL;
+    ramcrc_shard* sh = new (std::nothrow) ramcrc_shard();
+    if (!sh)
+        return RAMCRC_ENOMEM;
+    sh->nranks = nranks;
+    sh->local.resize(1);
+    Local& l = sh->local[0];
+    l.rank = rank;
+    l.device = device;
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof(u));
+    ncclResult_t e;
+    {
+        DevGuard g(device);
+        e = r->comm_init_rank(&l.comm, nranks, u, rank);
+    }
+    if (e != ncclSuccess) {
+        l.comm = nullptr;
+        delete sh;
+        return rccl_fail(r, e, "ncclCommInitRank");
+    }
+    int rc = finish_create(sh);
+    if (rc) {
+        ramcrc_shard_destroy(sh);
+        return rc;
+    }
+    *out = sh;
+    return RAMCRC_OK;
+}
+
+int ramcrc_shard_destroy(ramcrc_shard* sh)
+{
+    if (!sh)
+        return RAMCRC_OK;
+    const Rccl* r = rccl();
+    for (Local& l : sh->local) {
+        DevGuard g(l.device);
+        if (l.stream)
+            (void)hipStreamSynchronize(l.stream);
+        if (l.comm && r)
+            (void)r->comm_destroy(l.comm);
+        if (l.ctx)
+            ramcrc_ctx_destroy(l.ctx);
+        if (l.gather)
+            (void)hipFree(l.gather);
+        if (l.all)
+            (void)hipFree(l.all);
+        if (l.stream)
+            (void)hipStreamDestroy(l.stream);
+    }
+    delete sh;
+    return RAMCRC_OK;
+}
+
+int ramcrc_shard_local_count(const ramcrc_shard* sh)
+{
+    return sh ? int(sh->local.size()) : 0;
+}
+
+int ramcrc_shard_info(const ramcrc_shard* sh, int k, int* rank, int* device, void** stream,
+                      ramcrc_ctx** ctx)
+{
+    if (!sh || k < 0 || k >= int(sh->local.size()))
+        return RAMCRC_EINVAL;
+    const Local& l = sh->local[k];
+    if (rank) *rank = l.rank;
+    if (device) *device = l.device;
+    if (stream) *stream = l.stream;
+    if (ctx) *ctx = l.ctx;
+    return RAMCRC_OK;
+}
+
+int ramcrc_shard_segments(ramcrc_shard* sh, const void* const* d_shard, uint64_t seg_bytes,
+                          uint64_t nseg, uint32_t* const* d_all, uint32_t flags)
+{
+    if (!sh || !d_shard || seg_bytes == 0)
+        return RAMCRC_EINVAL;
+    const Rccl* r = rccl();
+    if (!r)
+        return RAMCRC_ERCCL;
+    std::lock_guard<std::mutex> lk(sh->mu);
+    const uint64_t N = uint64_t(sh->nranks);
+    const uint64_t width = (nseg + N - 1) / N;
+    const uint64_t base = nseg / N, rem = nseg % N;
+    if (width == 0) {
+        for (Local& l : sh->local)
+            l.last_nseg = 0;
+        return RAMCRC_OK;
+    }
+    // a uniform split lets the all-gather land directly in the caller's array
+    const bool direct = rem == 0 && d_all;
+    for (size_t k = 0; k < sh->local.size(); k++) {
+        Local& l = sh->local[k];
+        DevGuard g(l.device);
+        uint64_t lo = 0, hi = 0;
+        ramcrc_shard_range(nseg, sh->nranks, l.rank, &lo, &hi);
+        if (hi > lo && !d_shard[k])
+            return RAMCRC_EINVAL;
+        int rc = RAMCRC_OK;
+        if (!direct)
+            rc = grow(&l.gather, &l.gather_cap, width * N);
+        if (!rc && !d_all)
+            rc = grow(&l.all, &l.all_cap, nseg);
+        if (rc)
+            return rc;
+        uint32_t* recv = direct ? d_all[k] : l.gather;
+        rc = ramcrc_segments_device(l.ctx, d_shard[k], seg_bytes, hi - lo, nullptr,
+                                    recv + uint64_t(l.rank) * width, flags, l.stream);
+        if (rc)
+            return rc;
+        l.last_nseg = nseg;
+        l.last_internal = !d_all;
+    }
+    // one group: a single process driving several ranks must issue their
+    // collectives together (a lone rank's call would block on the others)
+    RCCLCHK(r, r->group_start(), "ncclGroupStart");
+    for (size_t k = 0; k < sh->local.size(); k++) {
+        Local& l = sh->local[k];
+        uint32_t* recv = direct ? d_all[k] : l.gather;
+        ncclResult_t e = r->all_gather(recv + uint64_t(l.rank) * width, recv, width, ncclUint32,
+                                       l.comm, l.stream);
+        if (e != ncclSuccess) {
+            (void)r->group_end();
+            return rccl_fail(r, e, "ncclAllGather");
+        }
+    }
+    RCCLCHK(r, r->group_end(), "ncclGroupEnd");
+    if (!direct) {
+        for (size_t k = 0; k < sh->local.size(); k++) {
+            Local& l = sh->local[k];
+            DevGuard g(l.device);
+            uint32_t* dst = d_all ? d_all[k] : l.all;
+            hipLaunchKernelGGL(k_unpad, dim3((nseg + 255) / 256), dim3(256), 0, l.stream,
+                               l.gather, dst, nseg, width, base, rem);
+            HIPCHK_S(hipGetLastError());
+        }
+    }
+    return RAMCRC_OK;
+}
+
+int ramcrc_shard_sync(ramcrc_shard* sh)
+{
+    if (!sh)
+        return RAMCRC_EINVAL;
+    const Rccl* r = rccl();
+    for (Local& l : sh->local) {
+        DevGuard g(l.device);
+        HIPCHK_S(hipStreamSynchronize(l.stream));
+        if (r && l.comm) {
+            ncclResult_t ae = ncclSuccess;
+            RCCLCHK(r, r->comm_async_error(l.comm, &ae), "ncclCommGetAsyncError");
+            if (ae != ncclSuccess)
+                return rccl_fail(r, ae, "RCCL asynchronous error");
+        }
+        int rc = ramcrc_ctx_check(l.ctx, l.stream);
+        if (rc)
+            return rc;
+    }
+    return RAMCRC_OK;
+}
+
+int ramcrc_shard_results(ramcrc_shard* sh, int k, uint32_t* h_out, uint64_t nseg)
+{
+    if (!sh || k < 0 || k >= int(sh->local.size()) || (nseg && !h_out))
+        return RAMCRC_EINVAL;
+    Local& l = sh->local[k];
+    if (!l.last_internal || nseg != l.last_nseg)
+        return RAMCRC_EINVAL;
+    if (nseg == 0)
+        return RAMCRC_OK;
+    DevGuard g(l.device);
+    HIPCHK_S(hipStreamSynchronize(l.stream));
+    HIPCHK_S(hipMemcpy(h_out, l.all, nseg * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return RAMCRC_OK;
+}
+
+}  // extern "C"

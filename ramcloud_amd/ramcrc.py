@@ -20,7 +20,7 @@ _lib = None
 FINALIZE = 1
 
 _ERRORS = {0: "ok", -1: "invalid argument", -2: "out of memory", -3: "HIP error",
-           -4: "no usable device", -5: "RCCL error"}
+           -4: "no usable device", -5: "RCCL error", -6: "launch refused (scratch too small)"}
 
 
 class RamcrcError(RuntimeError):
@@ -71,6 +71,20 @@ def lib():
         "ramcrc_ctx_set_timing": (i32, [vp, i32]),
         "ramcrc_ctx_scan_time": (i32, [vp, _c.POINTER(_c.c_double), _c.POINTER(u64)]),
         "ramcrc_ctx_status": (i32, [vp, _c.POINTER(u32)]),
+        "ramcrc_ctx_check": (i32, [vp, vp]),
+        "ramcrc_segment_fill_objects_device": (i32, [vp, vp, u64, u32, u64, u32, u64, vp, vp,
+                                                     _c.POINTER(u32)]),
+        "ramcrc_shard_unique_id": (i32, [vp]),
+        "ramcrc_shard_create_all": (i32, [vp, i32, _c.POINTER(vp)]),
+        "ramcrc_shard_create_rank": (i32, [vp, i32, i32, i32, _c.POINTER(vp)]),
+        "ramcrc_shard_destroy": (i32, [vp]),
+        "ramcrc_shard_range": (i32, [u64, i32, i32, _c.POINTER(u64), _c.POINTER(u64)]),
+        "ramcrc_shard_local_count": (i32, [vp]),
+        "ramcrc_shard_info": (i32, [vp, i32, _c.POINTER(i32), _c.POINTER(i32), _c.POINTER(vp),
+                                    _c.POINTER(vp)]),
+        "ramcrc_shard_segments": (i32, [vp, vp, u64, u64, vp, u32]),
+        "ramcrc_shard_sync": (i32, [vp]),
+        "ramcrc_shard_results": (i32, [vp, i32, vp, u64]),
         "ramcrc_stream_create_cu_mask": (i32, [i32, vp, u32, _c.POINTER(vp)]),
         "ramcrc_stream_destroy": (i32, [vp]),
         "ramcrc_ctx_set_cus": (i32, [vp, i32]),
@@ -238,6 +252,11 @@ class Context:
         _check(lib().ramcrc_ctx_status(self._h, _c.byref(s)), "ramcrc_ctx_status")
         return s.value
 
+    def check(self, stream=None):
+        """Wait for `stream`; raise if any launch of this context was refused
+        since the last check (ramcrc_ctx_check)."""
+        _check(lib().ramcrc_ctx_check(self._h, _stream(stream)), "ramcrc_ctx_check")
+
     def set_cus(self, ncu):
         """Size this context's persistent grids for ncu CUs (0 = all): for
         launches on a CU-masked stream (see cu_mask_stream)."""
@@ -287,6 +306,19 @@ class Context:
                                                 _ptr(status), _stream(stream))
         _check(rc, "ramcrc_verify_objects_device")
         return status
+
+    def fill_objects(self, data, seg_stride, capacity, nseg, value_len, first_key=0, certs=None):
+        """RecoverSegmentBenchmark-shaped object segments built in place on the
+        device (ramcrc_segment_fill_objects_device): returns (objects per
+        segment, segment_length, checksum); certs (int32 CUDA [nseg, 2]) gets
+        every segment's certificate when given.  Synchronous."""
+        cert = np.zeros(2, dtype=np.uint32)
+        per = _c.c_uint32(0)
+        rc = lib().ramcrc_segment_fill_objects_device(
+            self._h, _ptr(data), seg_stride, capacity, nseg, value_len, first_key, _ptr(certs),
+            _c.c_void_p(cert.ctypes.data), _c.byref(per))
+        _check(rc, "ramcrc_segment_fill_objects_device")
+        return per.value, int(cert[0]), int(cert[1])
 
     def assemble_objects(self, data, off, length, out=None, stream=None):
         """Object::assembleForLog's checksum for serialized objects in `data`
@@ -338,3 +370,110 @@ class Context:
                                       FINALIZE if finalize else 0, batch, depth)
         _check(rc, "ramcrc_stream_host")
         return out
+
+
+# ------------------------------------------------------------ multi-GPU shard
+def shard_range(nseg, nranks, rank):
+    """[lo, hi) of segment indices rank `rank` of `nranks` owns (ramcrc_shard_range)."""
+    lo, hi = _c.c_uint64(0), _c.c_uint64(0)
+    _check(lib().ramcrc_shard_range(nseg, nranks, rank, _c.byref(lo), _c.byref(hi)),
+           "ramcrc_shard_range")
+    return lo.value, hi.value
+
+
+def shard_unique_id():
+    """128-byte RCCL unique id for ramcrc_shard_create_rank (bytes)."""
+    buf = (_c.c_uint8 * 128)()
+    _check(lib().ramcrc_shard_unique_id(buf), "ramcrc_shard_unique_id")
+    return bytes(buf)
+
+
+class _StdoutToStderr:
+    """RCCL prints a version banner on stdout at communicator creation; a
+    benchmark's stdout carries exactly one JSON line, so point fd 1 at
+    stderr for the duration."""
+
+    def __enter__(self):
+        import sys
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
+class Shard:
+    """The recovery-scan shard of libramcrc (ramcrc_shard_*): scan of each
+    rank's contiguous segment range + one RCCL all-gather of the CRCs.
+
+    Shard(devices=[0, 1, ...])          one process, several GPUs (ncclCommInitAll)
+    Shard(uid=..., nranks=N, rank=r, device=d)   one process per GPU (ncclCommInitRank)
+    """
+
+    def __init__(self, devices=None, uid=None, nranks=None, rank=None, device=None):
+        h = _c.c_void_p()
+        if devices is not None:
+            arr = (_c.c_int * len(devices))(*devices)
+            with _StdoutToStderr():
+                rc = lib().ramcrc_shard_create_all(arr, len(devices), _c.byref(h))
+            _check(rc, "ramcrc_shard_create_all")
+        else:
+            if uid is None or len(uid) != 128:
+                raise RamcrcError("Shard needs devices=[...] or a 128-byte uid")
+            buf = (_c.c_uint8 * 128).from_buffer_copy(uid)
+            with _StdoutToStderr():
+                rc = lib().ramcrc_shard_create_rank(buf, int(nranks), int(rank), int(device),
+                                                    _c.byref(h))
+            _check(rc, "ramcrc_shard_create_rank")
+        self._h = h
+        self.nlocal = int(lib().ramcrc_shard_local_count(h))
+
+    def info(self, k=0):
+        """(rank, device, stream handle, ctx handle) of local rank k."""
+        r, d = _c.c_int(0), _c.c_int(0)
+        st, cx = _c.c_void_p(), _c.c_void_p()
+        _check(lib().ramcrc_shard_info(self._h, k, _c.byref(r), _c.byref(d), _c.byref(st),
+                                       _c.byref(cx)), "ramcrc_shard_info")
+        return r.value, d.value, st.value, cx.value
+
+    def set_timing(self, enable=True, k=0):
+        _check(lib().ramcrc_ctx_set_timing(_c.c_void_p(self.info(k)[3]), 1 if enable else 0),
+               "ramcrc_ctx_set_timing")
+
+    def scan_time(self, k=0):
+        ms, n = _c.c_double(0), _c.c_uint64(0)
+        _check(lib().ramcrc_ctx_scan_time(_c.c_void_p(self.info(k)[3]), _c.byref(ms), _c.byref(n)),
+               "ramcrc_ctx_scan_time")
+        return ms.value, n.value
+
+    def segments(self, shards, seg_bytes, nseg, outs=None, finalize=True):
+        """shards[k]: local rank k's segment range (CUDA uint8 tensor); outs[k]
+        (int32 CUDA [nseg]) or None for the shard's own buffers."""
+        if len(shards) != self.nlocal or (outs is not None and len(outs) != self.nlocal):
+            raise RamcrcError("one shard (and output) per local rank")
+        sp = (_c.c_void_p * self.nlocal)(*[t.data_ptr() if t is not None else 0 for t in shards])
+        op = None if outs is None else (_c.c_void_p * self.nlocal)(*[t.data_ptr() for t in outs])
+        _check(lib().ramcrc_shard_segments(self._h, sp, seg_bytes, nseg, op,
+                                           FINALIZE if finalize else 0), "ramcrc_shard_segments")
+
+    def sync(self):
+        _check(lib().ramcrc_shard_sync(self._h), "ramcrc_shard_sync")
+
+    def results(self, nseg, k=0):
+        out = np.zeros(nseg, dtype=np.uint32)
+        _check(lib().ramcrc_shard_results(self._h, k, _c.c_void_p(out.ctypes.data), nseg),
+               "ramcrc_shard_results")
+        return out
+
+    def close(self):
+        if self._h:
+            lib().ramcrc_shard_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -46,6 +46,7 @@ REPLAY_HEADER_BYTES = {LOG_ENTRY_TYPE_OBJ: 24, LOG_ENTRY_TYPE_OBJTOMB: 32,
 
 REPLAY_SEED = 0x5245504C   # "REPL": value bytes of segment i use seed REPLAY_SEED + i
 OBJECT_OVERHEAD = 24 + 1 + 2 + 8   # Object::Header + KeyCount + CumulativeKeyLength + key
+MIN_REPLAY_ENTRY = 1 + 1 + 12      # EntryHeader + 1 length byte + ObjectSafeVersion::Header
 
 
 def entry_bytes(value_len):
@@ -108,9 +109,14 @@ class RecoveryVerify:
         self.capacity = capacity
         self.stride = capacity if stride is None else stride
         if entries_cap is None:
-            # every entry is at least a header byte, a length byte and an
-            # object header: enough for any segment of objects
-            min_entry = entry_bytes(0) if min_entry is None else min_entry
+            # Every replayed record is at least a header byte, a length byte
+            # and its type's header; the smallest is a safe version (12 B,
+            # src/Object.h:402-427), so a table of capacity // 14 + 1 records
+            # per segment holds any segment of replayed records.  Callers that
+            # know their segments hold only larger entries pass entries_cap or
+            # min_entry; a walk that still overflows marks the segment
+            # TABLE_FULL (never OK) and check() raises.
+            min_entry = MIN_REPLAY_ENTRY if min_entry is None else min_entry
             entries_cap = nseg * (capacity // min_entry + 1)
         dev = torch.device("cuda", ctx.device)
         self.entries = torch.zeros((entries_cap, 4), dtype=torch.int32, device=dev)
@@ -128,6 +134,20 @@ class RecoveryVerify:
                                 self.obj_crc, self.status, stream=stream)
         return self.status
 
-    def verify(self, d_segments, d_certs, stream=None):
+    def verify(self, d_segments, d_certs, stream=None, check=False):
+        """Walk + per-record verify.  check=True waits for the stream and raises
+        if the record table overflowed (some segment not verified) or a launch
+        was refused."""
         self.walk(d_segments, d_certs, stream)
-        return self.verify_objects(d_segments, stream)
+        st = self.verify_objects(d_segments, stream)
+        if check:
+            self.check(stream)
+        return st
+
+    def check(self, stream=None):
+        self.ctx.check(stream)
+        n = int(self.n_entries.item())
+        if n > self.entries.shape[0]:
+            raise ramcrc.RamcrcError(
+                f"segment walk found {n} records but the table holds {self.entries.shape[0]}: "
+                "segments marked TABLE_FULL were not verified")

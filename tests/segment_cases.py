@@ -256,3 +256,27 @@ def build_replay_mix(oracle, golden, nseg=8, seed=77, cap=CAPACITY):
         _, ck, _, _ = oracle.check_metadata(s, pos, 0)
         certs[i] = (pos, ck)
     return buf, certs, bad, checked
+
+
+def tombstone_segments(oracle, nseg, cap, seed=99):
+    """nseg segments packed with ObjectTombstones of empty keys -- 34-byte
+    entries (EntryHeader, 1 length byte, 32-byte ObjectTombstone::Header,
+    src/Object.h:285-338), smaller than any object entry -- each with a valid
+    checksum (src/Object.cc:1042-1057).  Returns (buf, certs, counts)."""
+    rng = np.random.default_rng(seed)
+    buf = np.zeros(nseg * cap, np.uint8)
+    certs = np.zeros((nseg, 2), np.uint32)
+    counts = np.zeros(nseg, np.uint32)
+    for i in range(nseg):
+        s = _seg(buf, i, cap)
+        pos = 0
+        while pos + 34 <= cap:
+            hdr = rng.integers(0, 256, 28, dtype=np.uint8).tobytes()
+            tomb = hdr + int(oracle.crc32c(np.frombuffer(hdr, np.uint8))).to_bytes(4, "little")
+            e = _log_entry(segments.LOG_ENTRY_TYPE_OBJTOMB, tomb)
+            s[pos:pos + len(e)] = np.frombuffer(e, np.uint8)
+            pos += len(e)
+            counts[i] += 1
+        _, ck, _, _ = oracle.check_metadata(s, pos, 0)
+        certs[i] = (pos, ck)
+    return buf, certs, counts

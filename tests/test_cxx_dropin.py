@@ -70,7 +70,7 @@ def _build_replay_test(ramcrc, tmp_path):
     exe = tmp_path / "replay_test"
     libdir = os.path.dirname(ramcrc.lib_path())
     subprocess.check_call([
-        "/opt/rocm/bin/hipcc", "-std=c++17", "-O2", "-Wall", "-Werror",
+        "/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-O2", "-Wall", "-Werror",
         "-I" + os.path.join(ROOT, "tests", "cpp"),
         "-I" + os.path.join(ROOT, "include", "ramcloud"),
         "-I" + os.path.join(ROOT, "include"),

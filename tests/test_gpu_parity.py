@@ -245,3 +245,35 @@ def test_full_headline_batch(ctx, oracle_mod):
     del data
     want = oracle_mod.segments(host, 8 * MiB, nseg, threads=16)
     assert np.array_equal(got, want)
+
+
+def test_entries_config3_full(ctx, oracle_mod):
+    """BASELINE config 3 at its stated size: the 1,000,000-entry Zipf table
+    (100 B / 1 KiB / 4 KiB, packed unaligned), every CRC against the oracle,
+    through the small-entry path and the general batch path; plus the
+    per-object (off + 4, len - 4) variant replay uses."""
+    from ramcloud_amd import workloads
+    lens = workloads.entry_lengths(1_000_000)
+    offs = workloads.packed_offsets(lens)
+    host = workloads.splitmix_bytes_np(workloads.ENTRY_SEED, int(lens.sum()))
+    base = dev(host)
+    want = oracle_mod.entries(host, offs, lens)
+    for api in ("entries", "batch"):
+        assert np.array_equal(run_api(ctx, api, base, offs, lens, None, True), want), api
+    want4 = oracle_mod.entries(host, offs + 4, lens - 4)
+    assert np.array_equal(run_api(ctx, "entries", base, offs + 4, lens - 4, None, True), want4)
+    ctx.check()
+
+
+def test_stream_host_config5_8mib(ctx, oracle_mod):
+    """BASELINE config 5 shape: 64 pinned 8 MiB host segments streamed through
+    the GPU (H2D on the copy stream overlapped with the kernels), CRCs back
+    in host memory, against the oracle; also a ragged last batch."""
+    seg, nseg = 8 * MiB, 64
+    host = torch.empty(nseg * seg, dtype=torch.uint8).pin_memory()
+    host.numpy()[:] = oracle_mod.splitmix_bytes(21, seg * nseg)
+    want = oracle_mod.segments(host.numpy(), seg, nseg, threads=16)
+    got = ctx.stream_host(host, seg, nseg, batch=8, depth=3)
+    assert np.array_equal(got, want)
+    got = ctx.stream_host(host, seg, 61, batch=8, depth=2)
+    assert np.array_equal(got, want[:61])

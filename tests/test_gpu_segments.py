@@ -92,13 +92,45 @@ def test_walk_verify_strided_high_addresses(ramcrc, oracle_mod):
 
 @pytest.mark.gpu
 def test_walk_table_full_flag(ramcrc, oracle_mod):
-    """A table too small for the walk: records dropped, flagged, count still exact."""
+    """A table too small for the walk: records dropped and flagged, count still
+    exact; a segment that lost records is never reported OK (it was not
+    verified), the others are, and RecoveryVerify.check raises."""
+    import torch
     cap, nseg = 1 << 18, 4
     buf, certs, counts = segments.object_segments_host(nseg, cap, 100)
     status, n, table, crc = _run(ramcrc, buf, certs, nseg, cap, 100)
     assert n == counts.sum()
-    assert (status[:, 0] & segments.SEG_TABLE_FULL).any()
-    assert ((status[:, 0] & segments.SEG_OK) != 0).all()
+    full = (status[:, 0] & segments.SEG_TABLE_FULL) != 0
+    assert full.any()
+    assert ((status[full, 0] & segments.SEG_OK) == 0).all()
+    assert (status[~full, 0] == segments.SEG_OK).all()
+    assert np.array_equal(status[:, 1], certs[:, 1])   # the metadata checksum is still reported
+    ctx = ramcrc.Context(0)
+    rv = segments.RecoveryVerify(ctx, nseg, cap, entries_cap=100)
+    d = torch.from_numpy(buf).cuda()
+    dc = torch.from_numpy(np.ascontiguousarray(certs).view(np.int32)).cuda()
+    with pytest.raises(ramcrc.RamcrcError):
+        rv.verify(d, dc, check=True)
+
+
+@pytest.mark.gpu
+def test_walk_tombstone_only_default_table(ramcrc, oracle_mod, golden):
+    """Segments packed with short tombstones (34-byte entries, below the object
+    minimum the round-1 default table assumed) with the default table: every
+    record is walked and verified, no segment is TABLE_FULL."""
+    import torch
+    cap, nseg = 1 << 16, 8
+    buf, certs, counts = segment_cases.tombstone_segments(oracle_mod, nseg, cap)
+    ctx = ramcrc.Context(0)
+    rv = segments.RecoveryVerify(ctx, nseg, cap)
+    d = torch.from_numpy(buf).cuda()
+    dc = torch.from_numpy(np.ascontiguousarray(certs).view(np.int32)).cuda()
+    st = rv.verify(d, dc, check=True).cpu().numpy().view(np.uint32)
+    assert (st[:, 0] == segments.SEG_OK).all()
+    assert np.array_equal(st[:, 2], counts)
+    assert (st[:, 3] == 0).all()
+    exp_status, _, _ = segment_cases.oracle_walk(oracle_mod, buf, certs, nseg, cap=cap)
+    assert np.array_equal(st, exp_status)
 
 
 @pytest.mark.gpu
