@@ -598,6 +598,8 @@ def _replay_pipelined(args, ctx, d, dc, nseg, seg_bytes, cap):
     t_walk = torch.cuda.ExternalStream(s_walk.handle)
     t_scan = torch.cuda.ExternalStream(s_scan.handle)
     ctx_walk = ramcrc.Context(dev)
+    if args.serial_walk:
+        ctx_walk.set_serial_walk(True)
     ctx.set_cus(len(rest))
     bufs = [d, d.clone()]
     rvs = [segments.RecoveryVerify(ctx, nseg, seg_bytes, entries_cap=cap) for _ in range(2)]
@@ -657,6 +659,8 @@ def run_replay(args, ranks):
     import torch
     from ramcloud_amd import ramcrc, segments
     ctx = ramcrc.Context(ranks.local)
+    if args.serial_walk:
+        ctx.set_serial_walk(True)
     seg = args.seg_mib * MiB
     nseg = args.replay_nseg
     d = torch.empty(nseg * seg, dtype=torch.uint8, device="cuda")
@@ -708,6 +712,7 @@ def run_replay(args, ranks):
                                f"{args.value_len} B-value objects",
                    "pipeline": (f"walk on {args.walk_cus} CUs beside the scan of the previous batch"
                                 if args.walk_cus else "none"),
+                   "walk": "serial (one wave per segment)" if args.serial_walk else "parallel (64 KiB parts)",
                    "objects": int(counts.sum()), "object_bytes_checksummed": obj_bytes},
         "roofline": {"bound": "hbm", "kernel": "k_entries (object verify)",
                      "achieved": round(achieved, 1) if achieved else None,
@@ -859,6 +864,8 @@ def parse_args(argv=None):
     ap.add_argument("--walk-cus", type=int, default=0,
                     help="replay config: pipeline batches, walking on this many CUs "
                          "(a multiple of 8) beside the object scan on the rest; 0 = serial")
+    ap.add_argument("--serial-walk", action="store_true",
+                    help="replay config: one wavefront per segment walk (RAMCRC_OPT_SERIAL_WALK)")
     ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-t1", action="store_true", help="config 4 at N>1: skip the 1-GPU t1 run")

@@ -177,11 +177,11 @@ typedef struct ramcrc_seg_status {
 
 /* Segment::checkMetadataIntegrity (src/Segment.cc:758-800) for n_seg segments
  * at d_base + i*seg_stride, each of seg_capacity bytes (a multiple of 16; the
- * reference's segletBlocks.size() * segletSize), against d_certs[i].  One
- * wavefront walks each segment's length-prefixed entries.  Writes
- * d_status[i] and appends one ramcrc_seg_entry per complete entry to
- * d_entries (up to entries_cap; the order across segments is unspecified,
- * within a segment it is increasing).  *d_n_entries (device) receives the
+ * reference's segletBlocks.size() * segletSize), against d_certs[i].  The
+ * length-prefixed entries are walked in parallel over 64 KiB parts of every
+ * segment (see RAMCRC_OPT_SERIAL_WALK).  Writes d_status[i] and one
+ * ramcrc_seg_entry per complete entry to d_entries (up to entries_cap; the
+ * order across segments is unspecified, within a segment it is increasing).  *d_n_entries (device) receives the
  * number of entries walked (may exceed entries_cap: see TABLE_FULL).
  * d_base 16-byte aligned, seg_stride a multiple of 16.  Stream-ordered. */
 int ramcrc_segment_walk_device(ramcrc_ctx* ctx, const void* d_base, uint64_t seg_stride,
@@ -337,6 +337,17 @@ int ramcrc_assemble_objects_device(ramcrc_ctx* ctx, void* d_base, const uint64_t
  * Header::checksum written back into the host object.  Synchronous. */
 int ramcrc_assemble_objects_host(ramcrc_ctx* ctx, void* const* objs, const uint64_t* lens,
                                  uint64_t n);
+
+/* Context options.
+ *   RAMCRC_OPT_SERIAL_WALK  nonzero: ramcrc_segment_walk_device walks every
+ *                           segment with one wavefront (the chain followed
+ *                           hop by hop); 0 (default): the parallel walk,
+ *                           which finds the chain in every 64 KiB part of a
+ *                           segment at once and hands only anomalous segments
+ *                           (offset wraps) to the serial walker.  Both give
+ *                           identical results. */
+#define RAMCRC_OPT_SERIAL_WALK 1
+int ramcrc_ctx_set_option(ramcrc_ctx* ctx, int option, int64_t value);
 
 /* Kernel timing (for benchmarks): when enabled, every launch brackets its
  * byte-scan kernel (k_chunks, or k_entries on the small path) with HIP events

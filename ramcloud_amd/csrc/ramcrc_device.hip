@@ -87,6 +87,7 @@ struct alignas(16) DeviceTables {
     uint32_t xinv[1024];    // x^(-8 p)
     uint32_t pos[132][256]; // k_entries_tiny: row r = X^(r-3)(byte), rows 0..3 (m <= 0) zero
     uint32_t xmeta[5 * 64 + 1];   // k_seg_walk: x^(8d), d = 0 .. 320 (one batch of metadata)
+    uint32_t xbyte[4][256];       // x^(8 * b * 256^j): x^(8d) for any 32-bit d in 4 factors
 };
 
 constexpr DeviceTables make_device_tables()
@@ -119,6 +120,14 @@ constexpr DeviceTables make_device_tables()
     }
     for (int d = 0; d <= 5 * 64; d++)
         t.xmeta[d] = ramcrc::xpow8(uint64_t(d));
+    for (int j = 0; j < 4; j++) {
+        const uint32_t base = ramcrc::xpow8(uint64_t(1) << (8 * j));
+        uint32_t acc = ramcrc::kOne;
+        for (int b = 0; b < 256; b++) {
+            t.xbyte[j][b] = acc;
+            acc = ramcrc::mulmod(acc, base);
+        }
+    }
     return t;
 }
 
@@ -1584,6 +1593,14 @@ struct ramcrc_ctx {
     uint64_t d_stage_cap = 0;
     hipStream_t copy_stream = nullptr;
     hipStream_t compute_stream = nullptr;
+    // parallel segment walk scratch: per part results, per segment flags / bases
+    void* walk_parts = nullptr;
+    uint64_t walk_parts_cap = 0;
+    uint32_t* walk_fallback = nullptr;
+    uint64_t walk_fallback_cap = 0;
+    uint64_t* walk_base = nullptr;
+    uint64_t walk_base_cap = 0;
+    bool serial_walk = false;   // RAMCRC_OPT_SERIAL_WALK
     // benchmark timing of the scan kernels
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_used, ev_free;
@@ -1789,6 +1806,7 @@ struct WalkDesc {
     u32x4* entries;
     uint64_t cap;
     unsigned long long* n_entries;
+    const uint32_t* only;   // nullable: walk only the segments with only[seg] != 0
 };
 
 // CRC32C update by the m (1..4) bytes in the low end of v; t[j][b] = X^(j+1)(b).
@@ -1840,6 +1858,8 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
     const int lane = threadIdx.x;
 
     for (uint64_t seg = blockIdx.x; seg < w.nseg; seg += gridDim.x) {
+        if (w.only && !w.only[seg])
+            continue;   // walked by the parallel walk (uniform per workgroup)
         const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
         const ramcrc_seg_cert cert = w.certs[seg];
         uint32_t pos = 0, crc = 0xFFFFFFFFu, count = 0, flags = 0;
@@ -2008,6 +2028,589 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
             w.status[seg] = st;
         }
     }
+}
+
+// ------------------------------------------------- parallel segment walk
+// The walk of Segment::checkMetadataIntegrity (src/Segment.cc:758-800) is a
+// chain: entry i+1 starts where entry i's length says.  One wave chasing it
+// through a whole 8 MiB segment (k_seg_walk) is latency-bound at ~160 ns a
+// hop, and a 512-segment batch is only 512 chains.  Here every segment is cut
+// into 64 KiB parts and the chain is found in every part at once:
+//
+//  A0 k_walk_sync   per part k >= 1 (one wave): the first offset in the part
+//                   from which kSyncHops consecutive hops each land on a
+//                   header of a valid LogEntryType (src/LogEntryTypes.h:29-68,
+//                   type < 12) inside the segment -- a guess of where the
+//                   chain enters the part.  Candidates are tested 512 at a
+//                   time, all hops of all live candidates issued together.
+//  A  k_walk_parts  per part (one lane): the reference's walk from the guess
+//                   (part 0: from offset 0) until it leaves the part or
+//                   reaches min(certificate length, capacity): entries,
+//                   the raw CRC of their header + length bytes, exit offset.
+//  B  k_walk_fix    per segment (one wave): the true chain, part by part in
+//                   order.  A part is accepted when the chain arrives exactly
+//                   at its guess (the walk is deterministic, so its result is
+//                   then the reference's); a part the chain skips is ignored;
+//                   otherwise the part is walked again from the true offset.
+//                   The accepted parts' metadata CRCs are combined with
+//                   raw(0, A||B) = X^|B|(raw(0, A)) ^ raw(0, B), the status is
+//                   written and the segment's records are allocated.
+//  C  k_walk_emit   per accepted part (one lane): walk again, writing the
+//                   records in order at their final slots.
+// A segment whose chain wraps the reference's uint32_t offset (it would then
+// walk backwards, or forever) or needs too many re-walks is handed to the
+// serial walker k_seg_walk, which implements those semantics.  The result of
+// every segment -- flags, checksum, entry count, records -- equals the serial
+// walk's (tests/test_gpu_segments.py runs both against the oracle).
+constexpr uint32_t kPartShift = 16;                 // 64 KiB parts
+constexpr uint32_t kPartBytes = 1u << kPartShift;
+constexpr uint32_t kNoStart = 0xFFFFFFFFu;
+constexpr int kSyncHops = 6;                        // hops a guess must survive
+constexpr int kSyncPer = 8;                         // candidates per lane per round
+constexpr uint32_t kSyncRound = kSyncPer * kWaveSize;   // 512 candidates
+constexpr uint32_t kSyncSpan = 16384;               // candidate bytes searched per part
+constexpr uint32_t kRewalkBudget = 1u << 15;        // hops B may re-walk before falling back
+constexpr uint32_t kNumTypes = 12;                  // TOTAL_LOG_ENTRY_TYPES, src/LogEntryTypes.h:68
+// part flags
+constexpr uint32_t kPartWalked = 1u, kPartWrap = 2u, kPartOverrun = 4u, kPartEmit = 8u;
+
+struct PartRes {
+    uint32_t start;    // A0: guess (kNoStart: none); B: the true start of an emitting part
+    uint32_t exit;     // A: offset where the part's walk stopped
+    uint32_t count;    // A: entries (records)
+    uint32_t nmeta;    // A: header + length bytes checksummed
+    uint32_t raw;      // A: raw(0, those bytes)
+    uint32_t flags;    // kPart*
+    uint64_t rec;      // B: first record slot of the part
+    // A: after each of the first kHist entries: the next offset and the
+    // metadata bytes / raw CRC so far.  A guess that is not the chain's entry
+    // but hops onto it (a junk header whose length lands on a real header)
+    // is then cut at the meeting point instead of walked again.
+    uint32_t hist_off[4];
+    uint32_t hist_nmeta[4];
+    uint32_t hist_raw[4];
+};
+constexpr uint32_t kHist = 4;
+constexpr uint32_t kMeet = 4;   // hops k_walk_fix walks looking for a guessed chain
+
+struct PWalk {
+    const uint8_t* base;
+    uint64_t stride;
+    uint32_t capacity;
+    uint32_t nparts;
+    uint64_t nseg;
+    const ramcrc_seg_cert* certs;
+    ramcrc_seg_status* status;
+    u32x4* entries;
+    uint64_t cap;
+    unsigned long long* n_entries;
+    PartRes* parts;
+    uint32_t* fallback;   // per segment: nonzero = walked by k_seg_walk
+    uint64_t* seg_base;   // per segment: first record slot (B)
+};
+
+typedef const __attribute__((address_space(1))) uint32_t gu32;
+
+// The bytes from pos on (at least 5: the header and up to 4 length bytes), as
+// Segment::copyOut would give them: bytes at or past the capacity read 0.
+// Two aligned dword loads (pos < capacity, capacity % 16 == 0).
+__device__ __forceinline__ uint64_t seg_peek(uint64_t seg, uint32_t pos, uint32_t capacity)
+{
+    const uint32_t a = pos & ~3u;
+    const bool two = a + 4 < capacity;
+    const uint32_t w0 = *reinterpret_cast<gu32*>(seg + a);
+    uint32_t w1 = *reinterpret_cast<gu32*>(seg + (two ? a + 4 : a));
+    w1 = two ? w1 : 0u;
+    return ((uint64_t(w1) << 32) | w0) >> (8 * (pos & 3));
+}
+
+// One hop of the reference walk from a header read as q: the entry's metadata
+// byte count (1 + lengthBytes), payload length and the next offset (64-bit,
+// so that a uint32_t wrap is visible).
+struct Hop {
+    uint32_t mbytes, len;
+    uint64_t next;
+};
+
+__device__ __forceinline__ Hop hop_of(uint64_t q, uint32_t pos)
+{
+    const uint32_t t = (uint32_t(q) >> 6) & 3;   // getLengthBytes() - 1
+    const uint64_t mask = t == 3 ? 0xFFFFFFFFull : ((1ull << (8 * (t + 1))) - 1);
+    Hop h;
+    h.len = uint32_t((q >> 8) & mask);
+    h.mbytes = t + 2;
+    h.next = uint64_t(pos) + h.mbytes + h.len;
+    return h;
+}
+
+// raw CRC update by an entry's header + length bytes (2..5 of them, from q).
+__device__ __forceinline__ uint32_t meta_update(const uint32_t* tab, uint32_t c, uint64_t q,
+                                                uint32_t mbytes)
+{
+    c = crc_small(tab, c, uint32_t(q), mbytes < 4 ? mbytes : 4);
+    if (mbytes == 5)
+        c = crc_small(tab, c, uint32_t(q >> 32), 1);
+    return c;
+}
+
+// x^(8d) for any 32-bit d.
+__device__ __forceinline__ uint32_t xpow8_dev(uint32_t d)
+{
+    uint32_t r = ramcrc::kOne;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t b = (d >> (8 * j)) & 0xFF;
+        if (b)
+            r = r == ramcrc::kOne ? g_tab.xbyte[j][b] : mulmod_dev(r, g_tab.xbyte[j][b]);
+    }
+    return r;
+}
+
+__device__ __forceinline__ uint32_t walk_limit(const PWalk& w, uint64_t seg)
+{
+    const uint32_t len = w.certs[seg].segment_length;
+    return len < w.capacity ? len : w.capacity;
+}
+
+// A0: one wave per part k >= 1.  The part's first kSyncWin bytes are staged
+// in LDS, so most candidate hops (the true chain's included, for entries of
+// a few KiB) read LDS instead of waiting on global memory.
+constexpr uint32_t kSyncStage = 13312;               // staged bytes per wave (13 x 1 KiB)
+constexpr uint32_t kSyncWin = kSyncStage - 16;       // candidates / hops read from LDS below this
+constexpr int kSyncWaves = 4;                        // waves per workgroup
+
+// A hop a candidate chain may take: a header of a type the log writes
+// (src/LogEntryTypes.h:29-68: 1 .. TOTAL-1; INVALID = 0 only fills the
+// zeroed tail), length bytes in the canonical (shortest) form EntryHeader
+// writes (src/Segment.h:135-148), and an entry that ends inside the segment.
+__device__ __forceinline__ bool plausible(uint64_t q, const Hop& h, uint32_t capacity)
+{
+    const uint32_t type = uint32_t(q) & 0x3f;
+    const uint32_t t = h.mbytes - 2;   // lengthBytes - 1
+    const bool canon = t == 0 || ((h.len >> (8 * t)) != 0);
+    return type != 0 && type < kNumTypes && canon && h.next <= capacity;
+}
+
+__global__ __launch_bounds__(kSyncWaves * kWaveSize) void k_walk_sync(PWalk w)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t wins[kSyncWaves][kSyncStage];
+    const int lane = threadIdx.x & (kWaveSize - 1);
+    const int wv = threadIdx.x / kWaveSize;
+    uint8_t* win = wins[wv];
+    const uint64_t nwave = uint64_t(gridDim.x) * kSyncWaves;
+    const uint64_t total = w.nseg * w.nparts;
+    for (uint64_t i = uint64_t(blockIdx.x) * kSyncWaves + wv; i < total; i += nwave) {
+        const uint64_t seg = i / w.nparts;
+        const uint32_t k = uint32_t(i - seg * w.nparts);
+        if (k == 0)
+            continue;   // part 0 starts at offset 0
+        const uint32_t B = k << kPartShift;
+        const uint32_t limit = walk_limit(w, seg);
+        const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
+        uint64_t end64 = uint64_t(B) + kSyncSpan;
+        end64 = end64 < uint64_t(B) + kPartBytes ? end64 : uint64_t(B) + kPartBytes;
+        end64 = end64 < w.capacity ? end64 : w.capacity;
+        const uint32_t end = uint32_t(end64 < limit ? end64 : limit);
+        if (end <= B) {
+            if (lane == 0)
+                w.parts[i].start = kNoStart;
+            continue;
+        }
+        // stage [B, B + kSyncStage): bytes at or past the capacity are 0.
+        // All loads are issued before the first store (one memory latency,
+        // not one per 1 KiB); the LDS is wave-private.
+        {
+            u32x4 v[kSyncStage / 1024];
+#pragma unroll
+            for (uint32_t u = 0; u < kSyncStage / 1024; u++) {
+                const uint64_t a = uint64_t(B) + u * 1024 + uint32_t(lane) * 16;
+                v[u] = a + 16 <= w.capacity ? load16(sb + a) : u32x4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kSyncStage / 1024; u++)
+                *reinterpret_cast<u32x4*>(win + u * 1024 + uint32_t(lane) * 16) = v[u];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // stores land before the reads
+        auto peek = [&](uint32_t p) -> uint64_t {   // the bytes from p (>= B)
+            const uint32_t o = p - B;
+            if (o + 8 <= kSyncStage) {
+                const uint32_t* w32 = reinterpret_cast<const uint32_t*>(win + (o & ~3u));
+                return ((uint64_t(w32[1]) << 32) | w32[0]) >> (8 * (o & 3));
+            }
+            return seg_peek(sb, p, w.capacity);
+        };
+        // Rounds of 512 candidates from `from`; the first candidate whose
+        // chain survives kSyncHops plausible hops (or reaches the limit).
+        // LDS-only: a hop that leaves the staged window ends the candidate
+        // (no global round trip for any lane); otherwise beyond-window hops
+        // read global memory.
+        // Candidates in rounds of 512 from B.  A candidate survives when its
+        // chain makes kSyncHops plausible hops (or reaches the limit).  A
+        // junk header whose length happens to land on a real header survives
+        // too, and then skips the real entries it jumps over.  The real first
+        // entry h is two real entries ahead after two hops, while a junk chain
+        // that lands on the real chain only after skipping some of it is
+        // further ahead: the survivor whose second hop lands nearest is kept
+        // (ties: the lower candidate; a junk chain that wins has met the real
+        // chain within two entries, which k_walk_fix resolves in as many
+        // hops), and as no candidate past that position can beat it, the scan
+        // stops there.  LDS-only: a hop that
+        // leaves the staged window ends the candidate (no global round trip
+        // for any lane); otherwise beyond-window hops read global memory.
+        auto search = [&](bool lds_only, uint32_t to) -> uint32_t {
+            const uint32_t wend = B + kSyncWin;   // peeks below wend stay in LDS
+            uint64_t best = ~0ull;                // (first hop target << 32) | candidate
+            for (uint32_t c0 = B; c0 < to && c0 < uint32_t(best >> 32); c0 += kSyncRound) {
+                const uint32_t cl = c0 + uint32_t(lane) * kSyncPer;
+                uint32_t p[kSyncPer];
+                uint32_t alive = 0;
+                uint64_t key = ~0ull;
+#pragma unroll
+                for (int j = 0; j < kSyncPer; j++) {
+                    const uint32_t c = cl + j;
+                    const uint64_t q = peek(c);
+                    const Hop h = hop_of(q, c);
+                    p[j] = uint32_t(h.next);
+                    alive |= (c < to && plausible(q, h, w.capacity)) ? (1u << j) : 0u;
+                }
+                uint32_t second[kSyncPer];   // position after two hops: the selection key
+#pragma unroll
+                for (int j = 0; j < kSyncPer; j++)
+                    second[j] = p[j];
+                for (int hh = 1; hh < kSyncHops && __ballot(alive != 0); hh++) {
+#pragma unroll
+                    for (int j = 0; j < kSyncPer; j++) {
+                        if (((alive >> j) & 1) && p[j] < limit) {   // (at the limit the walk ends: keep)
+                            if (lds_only && p[j] >= wend) {
+                                alive &= ~(1u << j);
+                                continue;
+                            }
+                            const uint64_t q = peek(p[j]);
+                            const Hop h = hop_of(q, p[j]);
+                            if (plausible(q, h, w.capacity))
+                                p[j] = uint32_t(h.next);
+                            else
+                                alive &= ~(1u << j);
+                        }
+                        if (hh == 1)
+                            second[j] = p[j];
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < kSyncPer; j++) {
+                    const uint64_t kj = (uint64_t(second[j]) << 32) | (cl + j);
+                    key = ((alive >> j) & 1) && kj < key ? kj : key;
+                }
+#pragma unroll
+                for (int s = 1; s < kWaveSize; s <<= 1) {
+                    const uint32_t lo = __shfl_xor(uint32_t(key), s, kWaveSize);
+                    const uint32_t hi = __shfl_xor(uint32_t(key >> 32), s, kWaveSize);
+                    const uint64_t o = (uint64_t(hi) << 32) | lo;
+                    key = o < key ? o : key;
+                }
+                best = key < best ? key : best;
+            }
+            return best == ~0ull ? kNoStart : uint32_t(best);
+        };
+        // entries of up to ~2 KiB: found with LDS reads alone; longer ones
+        // (their chain leaves the window) by the general search
+        const uint32_t lds_to = B + kSyncWin - 8 < end ? B + kSyncWin - 8 : end;
+        uint32_t guess = search(true, lds_to);
+        if (guess == kNoStart)
+            guess = search(false, end);
+        if (lane == 0)
+            w.parts[i].start = guess;
+    }
+}
+
+// The reference walk from `pos` while pos < stop, as one lane: fills the part
+// result (count, metadata bytes and raw CRC, exit, wrap / overrun flags) and,
+// when rec != nullptr, writes the records (slot < cap) from slot `rec`.
+__device__ __forceinline__ void walk_lane(const PWalk& w, const uint32_t* tab, uint64_t seg,
+                                          uint64_t sb, uint32_t pos, uint32_t stop, PartRes& r,
+                                          uint64_t rec, uint32_t budget)
+{
+    uint32_t count = 0, nmeta = 0, raw = 0, flags = kPartWalked, hops = 0;
+    while (pos < stop) {
+        if (hops++ >= budget) {
+            flags |= kPartWrap;   // out of budget: the serial walker takes the segment
+            break;
+        }
+        const uint64_t q = seg_peek(sb, pos, w.capacity);
+        const Hop h = hop_of(q, pos);
+        raw = meta_update(tab, raw, q, h.mbytes);
+        nmeta += h.mbytes;
+        if (h.next > 0xFFFFFFFFull) {
+            flags |= kPartWrap;
+            break;
+        }
+        if (h.next > w.capacity) {
+            flags |= kPartOverrun;
+            break;
+        }
+        if (rec != ~0ull && rec + count < w.cap)
+            w.entries[rec + count] = u32x4{uint32_t(seg), pos, h.len, uint32_t(q) & 0xFF};
+        if (count < kHist) {
+            r.hist_off[count] = uint32_t(h.next);
+            r.hist_nmeta[count] = nmeta;
+            r.hist_raw[count] = raw;
+        }
+        count++;
+        pos = uint32_t(h.next);
+    }
+    r.exit = pos;
+    r.count = count;
+    r.nmeta = nmeta;
+    r.raw = raw;
+    r.flags = flags;
+}
+
+__device__ __forceinline__ void walk_tab_fill(uint32_t* tab)
+{
+    for (uint32_t t = threadIdx.x; t < 4 * 256; t += blockDim.x)
+        tab[t] = g_tab.pos[1 + kTinyRow0 + t / 256][t % 256];
+    __syncthreads();
+}
+
+// A: one lane per part.
+__global__ __launch_bounds__(256) void k_walk_parts(PWalk w)
+{
+    __shared__ uint32_t tab[4 * 256];
+    walk_tab_fill(tab);
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= w.nseg * w.nparts)
+        return;
+    const uint64_t seg = i / w.nparts;
+    const uint32_t k = uint32_t(i - seg * w.nparts);
+    const uint32_t B = k << kPartShift;
+    const uint32_t limit = walk_limit(w, seg);
+    const uint32_t start = k == 0 ? 0u : w.parts[i].start;
+    PartRes r = w.parts[i];
+    r.start = start;
+    if (start == kNoStart || B >= limit) {
+        r.flags = 0;
+        r.count = r.nmeta = r.raw = 0;
+        r.exit = start;
+    } else {
+        const uint32_t pend = uint32_t(uint64_t(B) + kPartBytes < w.capacity ? uint64_t(B) + kPartBytes
+                                                                             : w.capacity);
+        const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
+        walk_lane(w, tab, seg, sb, start, pend < limit ? pend : limit, r, ~0ull, kPartBytes);
+    }
+    w.parts[i] = r;
+}
+
+// B: one wave per segment.
+__global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
+{
+    __shared__ uint32_t tab[4 * 256];
+    walk_tab_fill(tab);
+    const int lane = threadIdx.x;
+    for (uint64_t seg = blockIdx.x; seg < w.nseg; seg += gridDim.x) {
+        const uint32_t limit = walk_limit(w, seg);
+        const ramcrc_seg_cert cert = w.certs[seg];
+        const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
+        PartRes* parts = w.parts + seg * w.nparts;
+        // The true chain (wave-uniform): pos, the metadata CRC so far (raw
+        // state from 0xFFFFFFFF), the records before the current part.
+        uint32_t pos = 0, crc = 0xFFFFFFFFu, count = 0, rewalk = 0;
+        bool overrun = false, fallback = false;
+        for (uint32_t k0 = 0; k0 < w.nparts && pos < limit && !overrun && !fallback; k0 += kWaveSize) {
+            const uint32_t k = k0 + uint32_t(lane);
+            PartRes r{};
+            if (k < w.nparts)
+                r = parts[k];
+            // Decide part by part; a part walked again is walked by every
+            // lane on the same addresses and kept by the part's lane.
+            const uint32_t jn = w.nparts - k0 < uint32_t(kWaveSize) ? w.nparts - k0 : kWaveSize;
+            for (uint32_t j = 0; j < jn; j++) {
+                if (pos >= limit || overrun || fallback)
+                    break;
+                const uint64_t Ej64 = (uint64_t(k0 + j) << kPartShift) + kPartBytes;
+                if (pos >= Ej64)
+                    continue;   // the chain jumps over this part
+                const uint32_t Ej = uint32_t(Ej64 < w.capacity ? Ej64 : w.capacity);
+                const uint32_t st = __builtin_amdgcn_readlane(r.start, j);
+                const uint32_t fl = __builtin_amdgcn_readlane(r.flags, j);
+                uint32_t xexit = 0, xcount = 0, xflags = 0;
+                bool have = false;
+                if (fl & kPartWalked) {
+                    if (st == pos) {
+                        xexit = __builtin_amdgcn_readlane(r.exit, j);
+                        xcount = __builtin_amdgcn_readlane(r.count, j);
+                        xflags = fl;
+                        have = true;
+                    } else {
+                        // Walk from pos (at most kMeet hops, wave-uniform) until the
+                        // chain meets the guessed one: at its start, or after its
+                        // m-th entry (then its first m + 1 entries are junk).
+                        const uint32_t gc = __builtin_amdgcn_readlane(r.count, j);
+                        uint32_t ho[kHist];
+#pragma unroll
+                        for (uint32_t m = 0; m < kHist; m++)
+                            ho[m] = __builtin_amdgcn_readlane(r.hist_off[m], j);
+                        const uint32_t stop = Ej < limit ? Ej : limit;
+                        uint32_t p = pos, wc = 0, wn = 0, wr = 0;
+                        for (uint32_t t = 0; t <= kMeet && !have; t++) {
+                            int cut = -2;   // -1: meets the guess itself; m: after entry m
+                            if (p == st)
+                                cut = -1;
+#pragma unroll
+                            for (int m = kHist - 1; m >= 0; m--)
+                                if (uint32_t(m) < gc && ho[m] == p)
+                                    cut = m;
+                            if (cut != -2) {
+                                // pos .. p walked here (wc entries), then the guess's
+                                // walk from p: its totals minus its junk prefix
+                                uint32_t pn = 0, pr = 0;
+#pragma unroll
+                                for (int m = 0; m < int(kHist); m++)
+                                    if (m == cut) {
+                                        pn = __builtin_amdgcn_readlane(r.hist_nmeta[m], j);
+                                        pr = __builtin_amdgcn_readlane(r.hist_raw[m], j);
+                                    }
+                                const uint32_t tn = __builtin_amdgcn_readlane(r.nmeta, j);
+                                const uint32_t tr = __builtin_amdgcn_readlane(r.raw, j);
+                                const uint32_t sn = tn - pn;   // suffix metadata bytes
+                                const uint32_t sr = cut >= 0 ? tr ^ mulmod_horner(pr, xpow8_dev(sn)) : tr;
+                                xexit = __builtin_amdgcn_readlane(r.exit, j);
+                                xcount = wc + gc - uint32_t(cut + 1);
+                                xflags = fl;
+                                const uint32_t nn = wn + sn;
+                                const uint32_t rr = mulmod_horner(wr, xpow8_dev(sn)) ^ sr;
+                                have = true;
+                                if (lane == int(j)) {
+                                    r.start = pos;
+                                    r.count = xcount;
+                                    r.nmeta = nn;
+                                    r.raw = rr;
+                                }
+                                break;
+                            }
+                            if (p >= stop)
+                                break;
+                            const uint64_t q = seg_peek(sb, p, w.capacity);
+                            const Hop h = hop_of(q, p);
+                            if (h.next > w.capacity)
+                                break;   // (an overrun or a wrap: the full walk below decides)
+                            wr = meta_update(tab, wr, q, h.mbytes);
+                            wn += h.mbytes;
+                            wc++;
+                            p = uint32_t(h.next);
+                        }
+                    }
+                }
+                if (!have) {
+                    // misguessed: walk this part again from the true offset
+                    const uint32_t stop = Ej < limit ? Ej : limit;
+                    PartRes x;
+                    walk_lane(w, tab, seg, sb, pos, stop, x, ~0ull,
+                              rewalk < kRewalkBudget ? kRewalkBudget - rewalk : 0u);
+                    rewalk += x.count + 1;
+                    xexit = x.exit;
+                    xcount = x.count;
+                    xflags = x.flags;
+                    if (lane == int(j)) {
+                        r.start = pos;
+                        r.exit = x.exit;
+                        r.count = x.count;
+                        r.nmeta = x.nmeta;
+                        r.raw = x.raw;
+                        r.flags = x.flags;
+                    }
+                }
+                if (xflags & kPartWrap) {
+                    fallback = true;
+                    break;
+                }
+                if (lane == int(j)) {
+                    r.flags |= kPartEmit;
+                    r.rec = count;   // relative to the segment's first record
+                }
+                count += xcount;
+                pos = xexit;
+                if (xflags & kPartOverrun)
+                    overrun = true;
+            }
+            if (fallback)
+                break;
+            // Fold the accepted parts of this chunk into crc in one step:
+            // crc <- X^n(crc) ^ sum_j X^(suffix_j)(raw_j), suffix_j = the
+            // metadata bytes of the accepted parts after j, n = all of them.
+            const bool acc = k < w.nparts && (r.flags & kPartEmit);
+            const uint32_t nm = acc ? r.nmeta : 0u;
+            uint32_t incl = nm;   // inclusive suffix sum over higher lanes
+#pragma unroll
+            for (int s = 1; s < kWaveSize; s <<= 1) {
+                const uint32_t y = __shfl_down(incl, s, kWaveSize);
+                if (lane + s < kWaveSize)
+                    incl += y;
+            }
+            const uint32_t n_all = __shfl(incl, 0, kWaveSize);
+            uint32_t c = acc ? mulmod_horner(r.raw, xpow8_dev(incl - nm)) : 0u;
+#pragma unroll
+            for (int s = 1; s < kWaveSize; s <<= 1)
+                c ^= __shfl_xor(c, s, kWaveSize);
+            crc = mulmod_horner(crc, xpow8_dev(n_all)) ^ c;
+            if (k < w.nparts)
+                parts[k] = r;
+        }
+        if (fallback) {
+            if (lane == 0)
+                w.fallback[seg] = 1;
+            continue;
+        }
+        uint32_t flags = 0;
+        const uint32_t fin = ~crc_small(tab, crc, cert.segment_length, 4);
+        if (overrun)
+            flags |= RAMCRC_SEG_PAST_CAPACITY;
+        else if (pos > cert.segment_length)
+            flags |= RAMCRC_SEG_PAST_LENGTH;
+        else if (fin != cert.checksum)
+            flags |= RAMCRC_SEG_BAD_CHECKSUM;
+        unsigned long long b = 0;
+        if (lane == 0 && count)
+            b = atomicAdd(w.n_entries, (unsigned long long)count);
+        b = __shfl(b, 0, kWaveSize);
+        if (b + count > w.cap)
+            flags |= RAMCRC_SEG_TABLE_FULL;
+        if (!(flags & (RAMCRC_SEG_PAST_CAPACITY | RAMCRC_SEG_PAST_LENGTH | RAMCRC_SEG_BAD_CHECKSUM |
+                       RAMCRC_SEG_TABLE_FULL)))
+            flags |= RAMCRC_SEG_OK;   // records dropped (TABLE_FULL): not verified, never OK
+        if (lane == 0) {
+            w.fallback[seg] = 0;
+            w.seg_base[seg] = b;
+            ramcrc_seg_status st;
+            st.flags = flags;
+            st.checksum = fin;
+            st.entries = count;
+            st.bad_objects = 0;
+            w.status[seg] = st;
+        }
+    }
+}
+
+// C: one lane per part the chain accepted.
+__global__ __launch_bounds__(256) void k_walk_emit(PWalk w)
+{
+    __shared__ uint32_t tab[4 * 256];
+    walk_tab_fill(tab);
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= w.nseg * w.nparts)
+        return;
+    const uint64_t seg = i / w.nparts;
+    const PartRes r = w.parts[i];
+    if (!(r.flags & kPartEmit) || w.fallback[seg])
+        return;
+    const uint32_t k = uint32_t(i - seg * w.nparts);
+    const uint32_t B = k << kPartShift;
+    const uint32_t limit = walk_limit(w, seg);
+    const uint32_t pend = uint32_t(uint64_t(B) + kPartBytes < w.capacity ? uint64_t(B) + kPartBytes
+                                                                         : w.capacity);
+    const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
+    PartRes x;
+    walk_lane(w, tab, seg, sb, r.start, pend < limit ? pend : limit, x, w.seg_base[seg] + r.rec,
+              kPartBytes);
 }
 
 // ObjectManager::replaySegment's checksum checks on the walk records of the
@@ -2236,6 +2839,9 @@ int ramcrc_ctx_destroy(ramcrc_ctx* c)
     if (c->sidx) (void)hipFree(c->sidx);
     if (c->sinit) (void)hipFree(c->sinit);
     if (c->obj_out) (void)hipFree(c->obj_out);
+    if (c->walk_parts) (void)hipFree(c->walk_parts);
+    if (c->walk_fallback) (void)hipFree(c->walk_fallback);
+    if (c->walk_base) (void)hipFree(c->walk_base);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -2259,6 +2865,17 @@ int ramcrc_ctx_reserve(ramcrc_ctx* c, uint64_t max_chunks, uint64_t max_entries)
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceGuard g(c->device);
     return reserve_locked(c, max_chunks, max_entries);
+}
+
+int ramcrc_ctx_set_option(ramcrc_ctx* c, int option, int64_t value)
+{
+    if (!c)
+        return RAMCRC_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    switch (option) {
+    case RAMCRC_OPT_SERIAL_WALK: c->serial_walk = value != 0; return RAMCRC_OK;
+    default: return RAMCRC_EINVAL;
+    }
 }
 
 int ramcrc_ctx_set_timing(ramcrc_ctx* c, int enable)
@@ -2636,9 +3253,54 @@ int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_s
     w.entries = reinterpret_cast<u32x4*>(d_entries);
     w.cap = entries_cap;
     w.n_entries = reinterpret_cast<unsigned long long*>(d_n_entries);
+    w.only = nullptr;
     uint64_t grid = n_seg;
     if (grid > uint64_t(64) * c->ncu)
         grid = uint64_t(64) * c->ncu;
+    if (!c->serial_walk) {
+        // parallel walk: sync search, part walks, per-segment fix-up, record
+        // emission; the serial walker then takes only the segments the fix-up
+        // handed back (uint32_t wraps, exhausted re-walk budget)
+        const uint32_t nparts = uint32_t((uint64_t(seg_capacity) + kPartBytes - 1) >> kPartShift);
+        const uint64_t total = n_seg * uint64_t(nparts);
+        int rc = grow_device(&c->walk_parts, &c->walk_parts_cap, total, sizeof(PartRes));
+        if (!rc)
+            rc = grow_device(reinterpret_cast<void**>(&c->walk_fallback), &c->walk_fallback_cap,
+                             n_seg, sizeof(uint32_t));
+        if (!rc)
+            rc = grow_device(reinterpret_cast<void**>(&c->walk_base), &c->walk_base_cap, n_seg,
+                             sizeof(uint64_t));
+        if (rc)
+            return rc;
+        PWalk pw{};
+        pw.base = w.base;
+        pw.stride = seg_stride;
+        pw.capacity = seg_capacity;
+        pw.nparts = nparts;
+        pw.nseg = n_seg;
+        pw.certs = d_certs;
+        pw.status = d_status;
+        pw.entries = w.entries;
+        pw.cap = entries_cap;
+        pw.n_entries = w.n_entries;
+        pw.parts = static_cast<PartRes*>(c->walk_parts);
+        pw.fallback = c->walk_fallback;
+        pw.seg_base = c->walk_base;
+        if (nparts > 1) {
+            uint64_t g0 = (total + kSyncWaves - 1) / kSyncWaves;
+            if (g0 > uint64_t(8) * c->ncu)
+                g0 = uint64_t(8) * c->ncu;
+            hipLaunchKernelGGL(k_walk_sync, dim3(g0), dim3(kSyncWaves * kWaveSize), 0, s, pw);
+            HIPCHK(hipGetLastError());
+        }
+        hipLaunchKernelGGL(k_walk_parts, dim3((total + 255) / 256), dim3(256), 0, s, pw);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_walk_fix, dim3(grid), dim3(kWaveSize), 0, s, pw);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_walk_emit, dim3((total + 255) / 256), dim3(256), 0, s, pw);
+        HIPCHK(hipGetLastError());
+        w.only = c->walk_fallback;
+    }
     hipLaunchKernelGGL(k_seg_walk, dim3(grid), dim3(kWaveSize), 0, s, w);
     HIPCHK(hipGetLastError());
     return RAMCRC_OK;

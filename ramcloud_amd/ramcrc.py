@@ -72,6 +72,7 @@ def lib():
         "ramcrc_ctx_scan_time": (i32, [vp, _c.POINTER(_c.c_double), _c.POINTER(u64)]),
         "ramcrc_ctx_status": (i32, [vp, _c.POINTER(u32)]),
         "ramcrc_ctx_check": (i32, [vp, vp]),
+        "ramcrc_ctx_set_option": (i32, [vp, i32, _c.c_int64]),
         "ramcrc_segment_fill_objects_device": (i32, [vp, vp, u64, u32, u64, u32, u64, vp, vp,
                                                      _c.POINTER(u32)]),
         "ramcrc_shard_unique_id": (i32, [vp]),
@@ -256,6 +257,11 @@ class Context:
         """Wait for `stream`; raise if any launch of this context was refused
         since the last check (ramcrc_ctx_check)."""
         _check(lib().ramcrc_ctx_check(self._h, _stream(stream)), "ramcrc_ctx_check")
+
+    def set_serial_walk(self, enable=True):
+        """Walk segments with one wavefront each (the serial chase) instead of
+        the parallel walk (RAMCRC_OPT_SERIAL_WALK)."""
+        _check(lib().ramcrc_ctx_set_option(self._h, 1, 1 if enable else 0), "ramcrc_ctx_set_option")
 
     def set_cus(self, ncu):
         """Size this context's persistent grids for ncu CUs (0 = all): for

@@ -16,10 +16,12 @@ def _sorted(table, extra=None):
     return table[order], (None if extra is None else extra[order])
 
 
-def _run(ramcrc, buf, certs, nseg, cap, entries_cap):
+def _run(ramcrc, buf, certs, nseg, cap, entries_cap, serial=False):
     import torch
 
     ctx = ramcrc.Context(0)
+    if serial:
+        ctx.set_serial_walk(True)
     d = torch.from_numpy(buf).cuda()
     dc = torch.from_numpy(np.ascontiguousarray(certs).view(np.int32)).cuda()
     rv = segments.RecoveryVerify(ctx, nseg, cap, entries_cap=entries_cap)
@@ -33,11 +35,18 @@ def _run(ramcrc, buf, certs, nseg, cap, entries_cap):
 
 
 @pytest.mark.gpu
-def test_walk_verify_damage_batch(ramcrc, oracle_mod):
+@pytest.mark.parametrize("serial", [False, True], ids=["parallel_walk", "serial_walk"])
+def test_walk_verify_damage_batch(ramcrc, oracle_mod, serial):
+    """Clean segments of value lengths 0 .. 200000 (entries larger than the
+    parallel walk's 64 KiB parts included), flipped values and checksums, bad
+    and short certificates, overruns, a uint32_t offset wrap, a cycle, an
+    empty segment, non-object and short-object entries, a certificate past
+    the last entry: every status, record and object CRC equals the oracle's,
+    with the parallel and the serial walker."""
     buf, certs, cases = segment_cases.build_batch(oracle_mod)
     nseg, cap = len(cases), segment_cases.CAPACITY
     exp_status, exp_table, exp_crc = segment_cases.oracle_walk(oracle_mod, buf, certs, nseg)
-    status, n, table, crc = _run(ramcrc, buf, certs, nseg, cap, nseg * (cap + 1))
+    status, n, table, crc = _run(ramcrc, buf, certs, nseg, cap, nseg * (cap + 1), serial)
     for i, c in enumerate(cases):
         assert np.array_equal(status[i], exp_status[i]), (c, status[i], exp_status[i])
     assert n == exp_table.shape[0]
@@ -131,6 +140,41 @@ def test_walk_tombstone_only_default_table(ramcrc, oracle_mod, golden):
     assert (st[:, 3] == 0).all()
     exp_status, _, _ = segment_cases.oracle_walk(oracle_mod, buf, certs, nseg, cap=cap)
     assert np.array_equal(st, exp_status)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("value_len", [64, 1024, 8192, 100000])
+def test_parallel_walk_8mib_vs_oracle(ramcrc, oracle_mod, value_len):
+    """8 MiB object segments (128 parts of the parallel walk) at the
+    RecoverSegmentBenchmark value sizes: entries from 101 B to larger than a
+    part; one segment with a damaged length in its middle (the chain derails:
+    every later part misguessed) and one with a wrong certificate.  Status,
+    records and object CRCs equal the oracle's and the serial walker's."""
+    import torch
+    cap, nseg = 8 << 20, 6
+    buf, certs, counts = segments.object_segments_host(nseg, cap, value_len, threads=8)
+    eb = segments.entry_bytes(value_len)
+    mid = (counts[1] // 2) * eb + cap   # segment 1: an entry in the middle claims 3 bytes more
+    lbx = (int(buf[mid]) >> 6) + 1
+    ln = int.from_bytes(bytes(buf[mid + 1:mid + 1 + lbx]), "little") + 3
+    buf[mid + 1:mid + 1 + lbx] = np.frombuffer(ln.to_bytes(4, "little")[:lbx], np.uint8)
+    certs[2, 1] ^= 0x10
+    exp_status, exp_table, exp_crc = segment_cases.oracle_walk(oracle_mod, buf, certs, nseg, cap=cap)
+    got = {}
+    for serial in (False, True):
+        status, n, table, crc = _run(ramcrc, buf, certs, nseg, cap, int(counts.sum()) * 2 + 1024,
+                                     serial)
+        assert np.array_equal(status, exp_status), (serial, status, exp_status)
+        assert n == exp_table.shape[0]
+        t_dev, c_dev = _sorted(table, crc)
+        t_exp, c_exp = _sorted(exp_table, exp_crc)
+        assert np.array_equal(t_dev, t_exp)
+        ok_seg = (exp_status[:, 0] & segments.SEG_OK) != 0
+        live = ((t_exp[:, 3] & 0x13F) == segments.LOG_ENTRY_TYPE_OBJ) & (t_exp[:, 2] >= 24) & ok_seg[t_exp[:, 0]]
+        assert np.array_equal(c_dev[live], c_exp[live])
+        got[serial] = status
+    assert (exp_status[[0, 3, 4, 5], 0] == segments.SEG_OK).all()
+    torch.cuda.synchronize()
 
 
 @pytest.mark.gpu
