@@ -1600,6 +1600,8 @@ struct ramcrc_ctx {
     uint64_t walk_fallback_cap = 0;
     uint64_t* walk_base = nullptr;
     uint64_t walk_base_cap = 0;
+    void* walk_recs = nullptr;
+    uint64_t walk_recs_cap = 0;
     bool serial_walk = false;   // RAMCRC_OPT_SERIAL_WALK
     // benchmark timing of the scan kernels
     bool timing = false;
@@ -2073,6 +2075,9 @@ constexpr uint32_t kRewalkBudget = 1u << 15;        // hops B may re-walk before
 constexpr uint32_t kNumTypes = 12;                  // TOTAL_LOG_ENTRY_TYPES, src/LogEntryTypes.h:68
 // part flags
 constexpr uint32_t kPartWalked = 1u, kPartWrap = 2u, kPartOverrun = 4u, kPartEmit = 8u;
+constexpr uint32_t kPartSpill = 16u;   // A: more records than its scratch holds
+constexpr uint32_t kPartChase = 32u;   // B: walked again; C walks it once more
+constexpr uint32_t kPartRec = 64;      // records A keeps per part (C copies them)
 
 struct PartRes {
     uint32_t start;    // A0: guess (kNoStart: none); B: the true start of an emitting part
@@ -2089,6 +2094,8 @@ struct PartRes {
     uint32_t hist_off[4];
     uint32_t hist_nmeta[4];
     uint32_t hist_raw[4];
+    uint32_t pre;      // B: entries walked before meeting the guessed chain (C walks them)
+    uint32_t cut;      // B: junk entries at the head of the guessed chain (C skips them)
 };
 constexpr uint32_t kHist = 4;
 constexpr uint32_t kMeet = 4;   // hops k_walk_fix walks looking for a guessed chain
@@ -2107,6 +2114,7 @@ struct PWalk {
     PartRes* parts;
     uint32_t* fallback;   // per segment: nonzero = walked by k_seg_walk
     uint64_t* seg_base;   // per segment: first record slot (B)
+    uint2* recs;          // per part: kPartRec records of A's walk {offset, length << 8 | header}
 };
 
 typedef const __attribute__((address_space(1))) uint32_t gu32;
@@ -2175,7 +2183,7 @@ __device__ __forceinline__ uint32_t walk_limit(const PWalk& w, uint64_t seg)
 // A0: one wave per part k >= 1.  The part's first kSyncWin bytes are staged
 // in LDS, so most candidate hops (the true chain's included, for entries of
 // a few KiB) read LDS instead of waiting on global memory.
-constexpr uint32_t kSyncStage = 13312;               // staged bytes per wave (13 x 1 KiB)
+constexpr uint32_t kSyncStage = 9216;                // staged bytes per wave (9 x 1 KiB)
 constexpr uint32_t kSyncWin = kSyncStage - 16;       // candidates / hops read from LDS below this
 constexpr int kSyncWaves = 4;                        // waves per workgroup
 
@@ -2239,11 +2247,6 @@ __global__ __launch_bounds__(kSyncWaves * kWaveSize) void k_walk_sync(PWalk w)
             }
             return seg_peek(sb, p, w.capacity);
         };
-        // Rounds of 512 candidates from `from`; the first candidate whose
-        // chain survives kSyncHops plausible hops (or reaches the limit).
-        // LDS-only: a hop that leaves the staged window ends the candidate
-        // (no global round trip for any lane); otherwise beyond-window hops
-        // read global memory.
         // Candidates in rounds of 512 from B.  A candidate survives when its
         // chain makes kSyncHops plausible hops (or reaches the limit).  A
         // junk header whose length happens to land on a real header survives
@@ -2253,62 +2256,111 @@ __global__ __launch_bounds__(kSyncWaves * kWaveSize) void k_walk_sync(PWalk w)
         // further ahead: the survivor whose second hop lands nearest is kept
         // (ties: the lower candidate; a junk chain that wins has met the real
         // chain within two entries, which k_walk_fix resolves in as many
-        // hops), and as no candidate past that position can beat it, the scan
-        // stops there.  LDS-only: a hop that
-        // leaves the staged window ends the candidate (no global round trip
-        // for any lane); otherwise beyond-window hops read global memory.
+        // hops).  h lies below the first hop of every survivor (a survivor
+        // before h jumps over it, h itself hops to the next real header), so
+        // the scan stops at the nearest first hop seen.
+        // Per round: lane l tests candidates c0 + 8 l + j (j < 8) on its
+        // first hop from three words it holds; the ~10 % that pass are
+        // compacted, one per lane, and chased level by level -- one peek per
+        // lane per level instead of a loop over eight slots.  LDS-only: a hop
+        // that leaves the staged window ends the candidate (no global round
+        // trip for any lane); otherwise beyond-window hops read global memory.
         auto search = [&](bool lds_only, uint32_t to) -> uint32_t {
             const uint32_t wend = B + kSyncWin;   // peeks below wend stay in LDS
-            uint64_t best = ~0ull;                // (first hop target << 32) | candidate
-            for (uint32_t c0 = B; c0 < to && c0 < uint32_t(best >> 32); c0 += kSyncRound) {
+            uint64_t best = ~0ull;                // (position after two hops << 32) | candidate
+            uint32_t bound = 0xFFFFFFFFu;         // nearest first hop of a survivor: h lies below it
+            for (uint32_t c0 = B; c0 < to && c0 < bound; c0 += kSyncRound) {
                 const uint32_t cl = c0 + uint32_t(lane) * kSyncPer;
-                uint32_t p[kSyncPer];
+                uint32_t d0, d1, d2;
+                {
+                    const uint64_t lo = peek(cl), hi = peek(cl + 4), hi2 = peek(cl + 8);
+                    d0 = uint32_t(lo);
+                    d1 = uint32_t(hi);
+                    d2 = uint32_t(hi2);
+                }
                 uint32_t alive = 0;
-                uint64_t key = ~0ull;
 #pragma unroll
                 for (int j = 0; j < kSyncPer; j++) {
                     const uint32_t c = cl + j;
-                    const uint64_t q = peek(c);
+                    const uint64_t w01 = (uint64_t(d1) << 32) | d0, w12 = (uint64_t(d2) << 32) | d1;
+                    const uint64_t q = (j < 4 ? w01 : w12) >> (8 * (j & 3));
                     const Hop h = hop_of(q, c);
-                    p[j] = uint32_t(h.next);
                     alive |= (c < to && plausible(q, h, w.capacity)) ? (1u << j) : 0u;
                 }
-                uint32_t second[kSyncPer];   // position after two hops: the selection key
-#pragma unroll
-                for (int j = 0; j < kSyncPer; j++)
-                    second[j] = p[j];
-                for (int hh = 1; hh < kSyncHops && __ballot(alive != 0); hh++) {
-#pragma unroll
-                    for (int j = 0; j < kSyncPer; j++) {
-                        if (((alive >> j) & 1) && p[j] < limit) {   // (at the limit the walk ends: keep)
-                            if (lds_only && p[j] >= wend) {
-                                alive &= ~(1u << j);
-                                continue;
-                            }
-                            const uint64_t q = peek(p[j]);
-                            const Hop h = hop_of(q, p[j]);
-                            if (plausible(q, h, w.capacity))
-                                p[j] = uint32_t(h.next);
-                            else
-                                alive &= ~(1u << j);
-                        }
-                        if (hh == 1)
-                            second[j] = p[j];
-                    }
-                }
+                // survivors, slot-major: mask[j] bit l = candidate c0 + 8 l + j
+                uint32_t cnt[kSyncPer];
+                uint64_t mask[kSyncPer];
+                uint32_t total = 0;
 #pragma unroll
                 for (int j = 0; j < kSyncPer; j++) {
-                    const uint64_t kj = (uint64_t(second[j]) << 32) | (cl + j);
-                    key = ((alive >> j) & 1) && kj < key ? kj : key;
+                    mask[j] = __ballot((alive >> j) & 1);
+                    cnt[j] = uint32_t(__popcll(mask[j]));
+                    total += cnt[j];
                 }
+                for (uint32_t t0 = 0; t0 < total; t0 += kWaveSize) {
+                    // lane -> its survivor: slot j, then the n-th set bit of mask[j]
+                    uint32_t n = t0 + uint32_t(lane);
+                    const bool have = n < total;
+                    uint64_t m = 0;
+                    uint32_t jj = 0;
 #pragma unroll
-                for (int s = 1; s < kWaveSize; s <<= 1) {
-                    const uint32_t lo = __shfl_xor(uint32_t(key), s, kWaveSize);
-                    const uint32_t hi = __shfl_xor(uint32_t(key >> 32), s, kWaveSize);
-                    const uint64_t o = (uint64_t(hi) << 32) | lo;
-                    key = o < key ? o : key;
+                    for (int j = 0; j < kSyncPer; j++) {
+                        const bool here = have && m == 0 && n < cnt[j];
+                        m = here ? mask[j] : m;
+                        jj = here ? uint32_t(j) : jj;
+                        n = (have && !here && m == 0) ? n - cnt[j] : n;
+                    }
+                    // n-th (0-based) set bit of m by halving
+                    uint32_t pos = 0;
+#pragma unroll
+                    for (int width = 32; width >= 1; width >>= 1) {
+                        const uint64_t lowmask = width == 64 ? ~0ull : ((1ull << width) - 1);
+                        const uint32_t c = uint32_t(__popcll((m >> pos) & lowmask));
+                        if (n >= c) {
+                            n -= c;
+                            pos += width;
+                        }
+                    }
+                    uint32_t c = cl - uint32_t(lane) * kSyncPer + pos * kSyncPer + jj;   // c0 + 8 pos + jj
+                    bool live = have;
+                    uint32_t p = c, first = 0, second = 0;
+                    for (int hh = 0; hh < kSyncHops && __ballot(live && p < limit); hh++) {
+                        if (live && p < limit) {   // (at the limit the walk ends: keep)
+                            if (hh > 0 && lds_only && p >= wend) {
+                                live = false;
+                            } else {
+                                const uint64_t q = peek(p);
+                                const Hop h = hop_of(q, p);
+                                if (plausible(q, h, w.capacity))
+                                    p = uint32_t(h.next);
+                                else
+                                    live = false;
+                            }
+                        }
+                        if (hh == 0)
+                            first = p;
+                        if (hh == 1)
+                            second = p;
+                    }
+                    if (second == 0)
+                        second = p;
+                    if (first == 0)
+                        first = p;
+                    uint64_t key = live ? ((uint64_t(second) << 32) | c) : ~0ull;
+                    uint32_t fb = live ? first : 0xFFFFFFFFu;
+#pragma unroll
+                    for (int s = 1; s < kWaveSize; s <<= 1)
+                        fb = min(fb, uint32_t(__shfl_xor(fb, s, kWaveSize)));
+                    bound = fb < bound ? fb : bound;
+#pragma unroll
+                    for (int s = 1; s < kWaveSize; s <<= 1) {
+                        const uint32_t lo = __shfl_xor(uint32_t(key), s, kWaveSize);
+                        const uint32_t hi = __shfl_xor(uint32_t(key >> 32), s, kWaveSize);
+                        const uint64_t o = (uint64_t(hi) << 32) | lo;
+                        key = o < key ? o : key;
+                    }
+                    best = key < best ? key : best;
                 }
-                best = key < best ? key : best;
             }
             return best == ~0ull ? kNoStart : uint32_t(best);
         };
@@ -2323,20 +2375,25 @@ __global__ __launch_bounds__(kSyncWaves * kWaveSize) void k_walk_sync(PWalk w)
     }
 }
 
-// The reference walk from `pos` while pos < stop, as one lane: fills the part
-// result (count, metadata bytes and raw CRC, exit, wrap / overrun flags) and,
-// when rec != nullptr, writes the records (slot < cap) from slot `rec`.
+// The reference walk from `pos` while pos < stop (at most `budget` hops), as
+// one lane: fills the part result (count, metadata bytes and raw CRC, exit,
+// wrap / overrun flags) and hands every record to sink(index, offset,
+// length, header byte).
+template <class Sink>
 __device__ __forceinline__ void walk_lane(const PWalk& w, const uint32_t* tab, uint64_t seg,
                                           uint64_t sb, uint32_t pos, uint32_t stop, PartRes& r,
-                                          uint64_t rec, uint32_t budget)
+                                          Sink&& sink, uint32_t budget)
 {
     uint32_t count = 0, nmeta = 0, raw = 0, flags = kPartWalked, hops = 0;
+    // The next header's load is issued before this entry's record store:
+    // vmcnt counts stores too, so a wait for a load issued after a store
+    // would also wait for the store to complete.
+    uint64_t q = pos < stop ? seg_peek(sb, pos, w.capacity) : 0ull;
     while (pos < stop) {
         if (hops++ >= budget) {
             flags |= kPartWrap;   // out of budget: the serial walker takes the segment
             break;
         }
-        const uint64_t q = seg_peek(sb, pos, w.capacity);
         const Hop h = hop_of(q, pos);
         raw = meta_update(tab, raw, q, h.mbytes);
         nmeta += h.mbytes;
@@ -2348,15 +2405,19 @@ __device__ __forceinline__ void walk_lane(const PWalk& w, const uint32_t* tab, u
             flags |= kPartOverrun;
             break;
         }
-        if (rec != ~0ull && rec + count < w.cap)
-            w.entries[rec + count] = u32x4{uint32_t(seg), pos, h.len, uint32_t(q) & 0xFF};
-        if (count < kHist) {
-            r.hist_off[count] = uint32_t(h.next);
-            r.hist_nmeta[count] = nmeta;
-            r.hist_raw[count] = raw;
-        }
+        const uint32_t next = uint32_t(h.next);
+        const uint64_t qn = next < stop ? seg_peek(sb, next, w.capacity) : 0ull;
+        sink(count, pos, h.len, uint32_t(q) & 0xFF);
+#pragma unroll
+        for (uint32_t m = 0; m < kHist; m++)   // (static indices: no scratch)
+            if (count == m) {
+                r.hist_off[m] = next;
+                r.hist_nmeta[m] = nmeta;
+                r.hist_raw[m] = raw;
+            }
         count++;
-        pos = uint32_t(h.next);
+        pos = next;
+        q = qn;
     }
     r.exit = pos;
     r.count = count;
@@ -2364,6 +2425,22 @@ __device__ __forceinline__ void walk_lane(const PWalk& w, const uint32_t* tab, u
     r.raw = raw;
     r.flags = flags;
 }
+
+struct NoSink {
+    __device__ void operator()(uint32_t, uint32_t, uint32_t, uint32_t) const {}
+};
+
+// Records straight to the table (slots below the table's capacity).
+struct TableSink {
+    u32x4* out;
+    uint64_t n;
+    uint32_t seg;
+    __device__ void operator()(uint32_t idx, uint32_t pos, uint32_t len, uint32_t hdr) const
+    {
+        if (idx < n)
+            out[idx] = u32x4{seg, pos, len, hdr};
+    }
+};
 
 __device__ __forceinline__ void walk_tab_fill(uint32_t* tab)
 {
@@ -2373,31 +2450,62 @@ __device__ __forceinline__ void walk_tab_fill(uint32_t* tab)
 }
 
 // A: one lane per part.
+// A keeps each lane's records (offset; length << 8 | header byte) in LDS
+// while it chases, then the wave writes them part by part with coalesced
+// stores: records stored by a lane one hop at a time would reach memory as
+// partial lines.  A part with more than kPartRec records, or an entry of
+// 16 MiB or more, is marked kPartSpill and walked again by C.
 __global__ __launch_bounds__(256) void k_walk_parts(PWalk w)
 {
     __shared__ uint32_t tab[4 * 256];
+    __shared__ uint2 lrec[256][kPartRec];
     walk_tab_fill(tab);
+    const int lane = threadIdx.x & (kWaveSize - 1);
     const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= w.nseg * w.nparts)
-        return;
-    const uint64_t seg = i / w.nparts;
-    const uint32_t k = uint32_t(i - seg * w.nparts);
-    const uint32_t B = k << kPartShift;
-    const uint32_t limit = walk_limit(w, seg);
-    const uint32_t start = k == 0 ? 0u : w.parts[i].start;
-    PartRes r = w.parts[i];
-    r.start = start;
-    if (start == kNoStart || B >= limit) {
-        r.flags = 0;
-        r.count = r.nmeta = r.raw = 0;
-        r.exit = start;
-    } else {
-        const uint32_t pend = uint32_t(uint64_t(B) + kPartBytes < w.capacity ? uint64_t(B) + kPartBytes
-                                                                             : w.capacity);
-        const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
-        walk_lane(w, tab, seg, sb, start, pend < limit ? pend : limit, r, ~0ull, kPartBytes);
+    const bool valid = i < w.nseg * w.nparts;
+    PartRes r{};
+    uint2* mine = lrec[threadIdx.x];
+    bool spill = false;
+    if (valid) {
+        const uint64_t seg = i / w.nparts;
+        const uint32_t k = uint32_t(i - seg * w.nparts);
+        const uint32_t B = k << kPartShift;
+        const uint32_t limit = walk_limit(w, seg);
+        r = w.parts[i];
+        const uint32_t start = k == 0 ? 0u : r.start;
+        r.start = start;
+        if (start == kNoStart || B >= limit) {
+            r.flags = 0;
+            r.count = r.nmeta = r.raw = 0;
+            r.exit = start;
+        } else {
+            const uint32_t pend = uint32_t(uint64_t(B) + kPartBytes < w.capacity
+                                               ? uint64_t(B) + kPartBytes : w.capacity);
+            const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
+            walk_lane(w, tab, seg, sb, start, pend < limit ? pend : limit, r,
+                      [&](uint32_t idx, uint32_t pos, uint32_t len, uint32_t hdr) {
+                          if (idx < kPartRec)
+                              mine[idx] = make_uint2(pos, (len << 8) | hdr);
+                          spill = spill || len >= (1u << 24);
+                      },
+                      kPartBytes);
+            if (r.count > kPartRec || spill)
+                r.flags |= kPartSpill;
+        }
+        w.parts[i] = r;
     }
-    w.parts[i] = r;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS records
+    const bool flush = valid && (r.flags & kPartWalked) && !(r.flags & kPartSpill);
+    uint64_t todo = __ballot(flush);
+    while (todo) {
+        const int j = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        const uint32_t n = __shfl(r.count, j, kWaveSize);
+        const uint64_t dst = (i - uint64_t(lane) + uint64_t(j)) * kPartRec;
+        const uint2* src = lrec[(threadIdx.x & ~63u) + uint32_t(j)];
+        for (uint32_t e = uint32_t(lane); e < n; e += kWaveSize)
+            w.recs[dst + e] = src[e];
+    }
 }
 
 // B: one wave per segment.
@@ -2415,7 +2523,85 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
         // state from 0xFFFFFFFF), the records before the current part.
         uint32_t pos = 0, crc = 0xFFFFFFFFu, count = 0, rewalk = 0;
         bool overrun = false, fallback = false;
-        for (uint32_t k0 = 0; k0 < w.nparts && pos < limit && !overrun && !fallback; k0 += kWaveSize) {
+        // Fold the accepted parts of a chunk (one per lane) into crc in one
+        // step: crc <- X^n(crc) ^ sum_j X^(suffix_j)(raw_j), suffix_j = the
+        // metadata bytes of the accepted parts after j, n = all of them.
+        auto fold = [&](bool acc, uint32_t nmeta, uint32_t raw) {
+            const uint32_t nm = acc ? nmeta : 0u;
+            uint32_t incl = nm;   // inclusive suffix sum over higher lanes
+#pragma unroll
+            for (int s = 1; s < kWaveSize; s <<= 1) {
+                const uint32_t y = __shfl_down(incl, s, kWaveSize);
+                if (lane + s < kWaveSize)
+                    incl += y;
+            }
+            const uint32_t n_all = __shfl(incl, 0, kWaveSize);
+            uint32_t c = acc ? mulmod_horner(raw, xpow8_dev(incl - nm)) : 0u;
+#pragma unroll
+            for (int s = 1; s < kWaveSize; s <<= 1)
+                c ^= __shfl_xor(c, s, kWaveSize);
+            crc = mulmod_horner(crc, xpow8_dev(n_all)) ^ c;
+        };
+        // Fast path -- every well-formed segment: part 0 starts at 0, every
+        // part below the limit was walked from exactly where the part before
+        // it stopped (inside itself), none wrapped and only the last may have
+        // overrun.  Checked for all parts at once, then accepted as walked.
+        const uint32_t nlive =
+            limit == 0 ? 0u : uint32_t((uint64_t(limit) + kPartBytes - 1) >> kPartShift);
+        bool fast = true;
+        {
+            uint32_t prev = 0;   // exit of the part before the chunk
+            for (uint32_t k0 = 0; k0 < nlive && fast; k0 += kWaveSize) {
+                const uint32_t k = k0 + uint32_t(lane);
+                const bool in = k < nlive;
+                uint32_t st = 0, ex = 0, fl = 0;
+                if (in) {
+                    st = parts[k].start;
+                    ex = parts[k].exit;
+                    fl = parts[k].flags;
+                }
+                uint32_t pe = __shfl_up(ex, 1, kWaveSize);
+                pe = lane == 0 ? prev : pe;
+                const uint64_t Ek = (uint64_t(k) << kPartShift) + kPartBytes;
+                const bool ok = !in || ((fl & kPartWalked) && !(fl & kPartWrap) && st == pe &&
+                                        uint64_t(pe) < Ek && (k + 1 == nlive || !(fl & kPartOverrun)));
+                fast = __ballot(!ok) == 0;
+                const uint32_t last = nlive - 1 - k0 < uint32_t(kWaveSize - 1) ? nlive - 1 - k0
+                                                                                : uint32_t(kWaveSize - 1);
+                prev = __shfl(ex, int(last), kWaveSize);
+            }
+        }
+        if (fast) {
+            for (uint32_t k0 = 0; k0 < nlive; k0 += kWaveSize) {
+                const uint32_t k = k0 + uint32_t(lane);
+                const bool in = k < nlive;
+                PartRes r{};
+                if (in)
+                    r = parts[k];
+                const uint32_t c = in ? r.count : 0u;
+                uint32_t incl = c;   // inclusive prefix of the record counts
+#pragma unroll
+                for (int s = 1; s < kWaveSize; s <<= 1) {
+                    const uint32_t y = __shfl_up(incl, s, kWaveSize);
+                    if (lane >= s)
+                        incl += y;
+                }
+                fold(in, r.nmeta, r.raw);
+                const uint32_t last = nlive - 1 - k0 < uint32_t(kWaveSize - 1) ? nlive - 1 - k0
+                                                                                : uint32_t(kWaveSize - 1);
+                if (in) {
+                    r.rec = count + incl - c;
+                    r.flags |= kPartEmit;
+                    r.pre = r.cut = 0;
+                    parts[k] = r;
+                }
+                count += __shfl(incl, int(last), kWaveSize);
+                pos = __shfl(r.exit, int(last), kWaveSize);
+                overrun = (__shfl(r.flags, int(last), kWaveSize) & kPartOverrun) != 0;
+            }
+        }
+        for (uint32_t k0 = 0; !fast && k0 < w.nparts && pos < limit && !overrun && !fallback;
+             k0 += kWaveSize) {
             const uint32_t k = k0 + uint32_t(lane);
             PartRes r{};
             if (k < w.nparts)
@@ -2484,6 +2670,8 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
                                     r.count = xcount;
                                     r.nmeta = nn;
                                     r.raw = rr;
+                                    r.pre = wc;
+                                    r.cut = uint32_t(cut + 1);
                                 }
                                 break;
                             }
@@ -2504,7 +2692,7 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
                     // misguessed: walk this part again from the true offset
                     const uint32_t stop = Ej < limit ? Ej : limit;
                     PartRes x;
-                    walk_lane(w, tab, seg, sb, pos, stop, x, ~0ull,
+                    walk_lane(w, tab, seg, sb, pos, stop, x, NoSink{},
                               rewalk < kRewalkBudget ? kRewalkBudget - rewalk : 0u);
                     rewalk += x.count + 1;
                     xexit = x.exit;
@@ -2516,7 +2704,7 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
                         r.count = x.count;
                         r.nmeta = x.nmeta;
                         r.raw = x.raw;
-                        r.flags = x.flags;
+                        r.flags = x.flags | kPartChase;
                     }
                 }
                 if (xflags & kPartWrap) {
@@ -2526,6 +2714,8 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
                 if (lane == int(j)) {
                     r.flags |= kPartEmit;
                     r.rec = count;   // relative to the segment's first record
+                    if (st == pos && (fl & kPartWalked))
+                        r.pre = r.cut = 0;   // accepted as walked
                 }
                 count += xcount;
                 pos = xexit;
@@ -2534,24 +2724,7 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
             }
             if (fallback)
                 break;
-            // Fold the accepted parts of this chunk into crc in one step:
-            // crc <- X^n(crc) ^ sum_j X^(suffix_j)(raw_j), suffix_j = the
-            // metadata bytes of the accepted parts after j, n = all of them.
-            const bool acc = k < w.nparts && (r.flags & kPartEmit);
-            const uint32_t nm = acc ? r.nmeta : 0u;
-            uint32_t incl = nm;   // inclusive suffix sum over higher lanes
-#pragma unroll
-            for (int s = 1; s < kWaveSize; s <<= 1) {
-                const uint32_t y = __shfl_down(incl, s, kWaveSize);
-                if (lane + s < kWaveSize)
-                    incl += y;
-            }
-            const uint32_t n_all = __shfl(incl, 0, kWaveSize);
-            uint32_t c = acc ? mulmod_horner(r.raw, xpow8_dev(incl - nm)) : 0u;
-#pragma unroll
-            for (int s = 1; s < kWaveSize; s <<= 1)
-                c ^= __shfl_xor(c, s, kWaveSize);
-            crc = mulmod_horner(crc, xpow8_dev(n_all)) ^ c;
+            fold(k < w.nparts && (r.flags & kPartEmit), r.nmeta, r.raw);
             if (k < w.nparts)
                 parts[k] = r;
         }
@@ -2590,27 +2763,68 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
     }
 }
 
-// C: one lane per part the chain accepted.
+// C: the records of every accepted part at their final slots.  A part
+// accepted as walked (the common case) already has its records in the
+// scratch A wrote: the wave copies them, part after part, 64 records per
+// instruction.  Entries walked by k_walk_fix before it met the guessed chain
+// are walked once more here (at most kMeet); parts walked again, or with more
+// records than the scratch holds, are walked again here in full.
 __global__ __launch_bounds__(256) void k_walk_emit(PWalk w)
 {
     __shared__ uint32_t tab[4 * 256];
     walk_tab_fill(tab);
     const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const bool valid = i < w.nseg * w.nparts;
+    const uint64_t seg = valid ? i / w.nparts : 0;
+    PartRes r{};
+    bool emit = false;
+    uint64_t slot = 0;
+    if (valid) {
+        r = w.parts[i];
+        emit = (r.flags & kPartEmit) && !w.fallback[seg];
+        if (emit)
+            slot = w.seg_base[seg] + r.rec;
+    }
+    const bool chase = emit && (r.flags & (kPartChase | kPartSpill));
+    const uint32_t pre = emit && !chase ? r.pre : 0u;
+    if (chase || pre) {
+        const uint32_t k = uint32_t(i - seg * w.nparts);
+        const uint32_t B = k << kPartShift;
+        const uint32_t limit = walk_limit(w, seg);
+        const uint32_t pend = uint32_t(uint64_t(B) + kPartBytes < w.capacity ? uint64_t(B) + kPartBytes
+                                                                             : w.capacity);
+        const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
+        PartRes x;
+        walk_lane(w, tab, seg, sb, r.start, pend < limit ? pend : limit, x,
+                  TableSink{w.entries + slot, slot < w.cap ? w.cap - slot : 0, uint32_t(seg)},
+                  chase ? kPartBytes : pre);
+    }
+}
+
+// C': the scratch records of the parts accepted without a second walk, one
+// thread per record slot (consecutive threads copy consecutive records).
+__global__ __launch_bounds__(256) void k_walk_copy(PWalk w)
+{
+    const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t i = t / kPartRec;
+    const uint32_t e = uint32_t(t - i * kPartRec);
     if (i >= w.nseg * w.nparts)
         return;
-    const uint64_t seg = i / w.nparts;
-    const PartRes r = w.parts[i];
-    if (!(r.flags & kPartEmit) || w.fallback[seg])
+    const PartRes& r = w.parts[i];
+    const uint32_t fl = r.flags;
+    if (!(fl & kPartEmit) || (fl & (kPartChase | kPartSpill)))
         return;
-    const uint32_t k = uint32_t(i - seg * w.nparts);
-    const uint32_t B = k << kPartShift;
-    const uint32_t limit = walk_limit(w, seg);
-    const uint32_t pend = uint32_t(uint64_t(B) + kPartBytes < w.capacity ? uint64_t(B) + kPartBytes
-                                                                         : w.capacity);
-    const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
-    PartRes x;
-    walk_lane(w, tab, seg, sb, r.start, pend < limit ? pend : limit, x, w.seg_base[seg] + r.rec,
-              kPartBytes);
+    const uint32_t n = r.count - r.pre;
+    if (e >= n)
+        return;
+    const uint64_t seg = i / w.nparts;
+    if (w.fallback[seg])
+        return;
+    const uint64_t dst = w.seg_base[seg] + r.rec + r.pre + e;
+    if (dst < w.cap) {
+        const uint2 v = w.recs[i * kPartRec + r.cut + e];
+        w.entries[dst] = u32x4{uint32_t(seg), v.x, v.y >> 8, v.y & 0xFF};
+    }
 }
 
 // ObjectManager::replaySegment's checksum checks on the walk records of the
@@ -2842,6 +3056,7 @@ int ramcrc_ctx_destroy(ramcrc_ctx* c)
     if (c->walk_parts) (void)hipFree(c->walk_parts);
     if (c->walk_fallback) (void)hipFree(c->walk_fallback);
     if (c->walk_base) (void)hipFree(c->walk_base);
+    if (c->walk_recs) (void)hipFree(c->walk_recs);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -3270,6 +3485,8 @@ int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_s
         if (!rc)
             rc = grow_device(reinterpret_cast<void**>(&c->walk_base), &c->walk_base_cap, n_seg,
                              sizeof(uint64_t));
+        if (!rc)
+            rc = grow_device(&c->walk_recs, &c->walk_recs_cap, total * kPartRec, sizeof(uint2));
         if (rc)
             return rc;
         PWalk pw{};
@@ -3286,6 +3503,7 @@ int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_s
         pw.parts = static_cast<PartRes*>(c->walk_parts);
         pw.fallback = c->walk_fallback;
         pw.seg_base = c->walk_base;
+        pw.recs = static_cast<uint2*>(c->walk_recs);
         if (nparts > 1) {
             uint64_t g0 = (total + kSyncWaves - 1) / kSyncWaves;
             if (g0 > uint64_t(8) * c->ncu)
@@ -3298,6 +3516,8 @@ int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_s
         hipLaunchKernelGGL(k_walk_fix, dim3(grid), dim3(kWaveSize), 0, s, pw);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_walk_emit, dim3((total + 255) / 256), dim3(256), 0, s, pw);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_walk_copy, dim3((total * kPartRec + 255) / 256), dim3(256), 0, s, pw);
         HIPCHK(hipGetLastError());
         w.only = c->walk_fallback;
     }
