@@ -2087,18 +2087,9 @@ struct PartRes {
     uint32_t raw;      // A: raw(0, those bytes)
     uint32_t flags;    // kPart*
     uint64_t rec;      // B: first record slot of the part
-    // A: after each of the first kHist entries: the next offset and the
-    // metadata bytes / raw CRC so far.  A guess that is not the chain's entry
-    // but hops onto it (a junk header whose length lands on a real header)
-    // is then cut at the meeting point instead of walked again.
-    uint32_t hist_off[4];
-    uint32_t hist_nmeta[4];
-    uint32_t hist_raw[4];
     uint32_t pre;      // B: entries walked before meeting the guessed chain (C walks them)
     uint32_t cut;      // B: junk entries at the head of the guessed chain (C skips them)
 };
-constexpr uint32_t kHist = 4;
-constexpr uint32_t kMeet = 4;   // hops k_walk_fix walks looking for a guessed chain
 
 struct PWalk {
     const uint8_t* base;
@@ -2408,13 +2399,6 @@ __device__ __forceinline__ void walk_lane(const PWalk& w, const uint32_t* tab, u
         const uint32_t next = uint32_t(h.next);
         const uint64_t qn = next < stop ? seg_peek(sb, next, w.capacity) : 0ull;
         sink(count, pos, h.len, uint32_t(q) & 0xFF);
-#pragma unroll
-        for (uint32_t m = 0; m < kHist; m++)   // (static indices: no scratch)
-            if (count == m) {
-                r.hist_off[m] = next;
-                r.hist_nmeta[m] = nmeta;
-                r.hist_raw[m] = raw;
-            }
         count++;
         pos = next;
         q = qn;
@@ -2627,65 +2611,101 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
                         xflags = fl;
                         have = true;
                     } else {
-                        // Walk from pos (at most kMeet hops, wave-uniform) until the
-                        // chain meets the guessed one: at its start, or after its
-                        // m-th entry (then its first m + 1 entries are junk).
+                        // Walk from pos (wave-uniform) until the chain meets the
+                        // guessed one: at one of the offsets A recorded for it
+                        // (lane e holds its e-th entry; the first is the guess);
+                        // its entries from there on are the true chain's.  Without
+                        // a meeting the walk covers the part (a full re-walk).
                         const uint32_t gc = __builtin_amdgcn_readlane(r.count, j);
-                        uint32_t ho[kHist];
-#pragma unroll
-                        for (uint32_t m = 0; m < kHist; m++)
-                            ho[m] = __builtin_amdgcn_readlane(r.hist_off[m], j);
+                        const uint32_t gn = gc < kPartRec ? gc : kPartRec;
+                        const uint64_t pidx = uint64_t(seg) * w.nparts + k0 + j;
+                        uint2 g = make_uint2(0xFFFFFFFFu, 0u);
+                        if (uint32_t(lane) < gn)
+                            g = w.recs[pidx * kPartRec + uint32_t(lane)];
                         const uint32_t stop = Ej < limit ? Ej : limit;
-                        uint32_t p = pos, wc = 0, wn = 0, wr = 0;
-                        for (uint32_t t = 0; t <= kMeet && !have; t++) {
-                            int cut = -2;   // -1: meets the guess itself; m: after entry m
-                            if (p == st)
-                                cut = -1;
-#pragma unroll
-                            for (int m = kHist - 1; m >= 0; m--)
-                                if (uint32_t(m) < gc && ho[m] == p)
-                                    cut = m;
-                            if (cut != -2) {
-                                // pos .. p walked here (wc entries), then the guess's
-                                // walk from p: its totals minus its junk prefix
-                                uint32_t pn = 0, pr = 0;
-#pragma unroll
-                                for (int m = 0; m < int(kHist); m++)
-                                    if (m == cut) {
-                                        pn = __builtin_amdgcn_readlane(r.hist_nmeta[m], j);
-                                        pr = __builtin_amdgcn_readlane(r.hist_raw[m], j);
-                                    }
-                                const uint32_t tn = __builtin_amdgcn_readlane(r.nmeta, j);
-                                const uint32_t tr = __builtin_amdgcn_readlane(r.raw, j);
-                                const uint32_t sn = tn - pn;   // suffix metadata bytes
-                                const uint32_t sr = cut >= 0 ? tr ^ mulmod_horner(pr, xpow8_dev(sn)) : tr;
-                                xexit = __builtin_amdgcn_readlane(r.exit, j);
-                                xcount = wc + gc - uint32_t(cut + 1);
-                                xflags = fl;
-                                const uint32_t nn = wn + sn;
-                                const uint32_t rr = mulmod_horner(wr, xpow8_dev(sn)) ^ sr;
-                                have = true;
-                                if (lane == int(j)) {
-                                    r.start = pos;
-                                    r.count = xcount;
-                                    r.nmeta = nn;
-                                    r.raw = rr;
-                                    r.pre = wc;
-                                    r.cut = uint32_t(cut + 1);
-                                }
+                        const uint32_t budget = rewalk < kRewalkBudget ? kRewalkBudget - rewalk : 0u;
+                        uint32_t p = pos, wc = 0, wn = 0, wr = 0, wflags = kPartWalked;
+                        int cut = -1;
+                        while (true) {
+                            const uint64_t hit = __ballot(uint32_t(lane) < gn && g.x == p);
+                            if (hit || (gn == 0 && p == st)) {
+                                cut = hit ? int(__builtin_ctzll(hit)) : 0;
                                 break;
                             }
                             if (p >= stop)
                                 break;
+                            if (wc >= budget) {
+                                wflags |= kPartWrap;   // out of budget: the serial walker
+                                break;
+                            }
                             const uint64_t q = seg_peek(sb, p, w.capacity);
                             const Hop h = hop_of(q, p);
-                            if (h.next > w.capacity)
-                                break;   // (an overrun or a wrap: the full walk below decides)
                             wr = meta_update(tab, wr, q, h.mbytes);
                             wn += h.mbytes;
+                            if (h.next > 0xFFFFFFFFull) {
+                                wflags |= kPartWrap;
+                                break;
+                            }
+                            if (h.next > w.capacity) {
+                                wflags |= kPartOverrun;
+                                break;
+                            }
                             wc++;
                             p = uint32_t(h.next);
                         }
+                        rewalk += wc + 1;
+                        if (cut >= 0) {
+                            // the guess's totals minus its first `cut` entries, whose
+                            // header + length bytes are folded from the records:
+                            // raw(0, A||S) = X^|S|(raw(0, A)) ^ raw(0, S)
+                            const bool in = lane < cut;
+                            const uint32_t mb = in ? ((g.y >> 6) & 3) + 2 : 0u;
+                            const uint64_t qe = uint64_t(g.y & 0xFF) | (uint64_t(g.y >> 8) << 8);
+                            const uint32_t re = in ? meta_update(tab, 0u, qe, mb) : 0u;
+                            uint32_t incl = mb;   // suffix sums of the prefix's bytes
+#pragma unroll
+                            for (int s = 1; s < kWaveSize; s <<= 1) {
+                                const uint32_t y = __shfl_down(incl, s, kWaveSize);
+                                if (lane + s < kWaveSize)
+                                    incl += y;
+                            }
+                            const uint32_t pn = __shfl(incl, 0, kWaveSize);
+                            uint32_t pr = in ? mulmod_horner(re, xpow8_dev(incl - mb)) : 0u;
+#pragma unroll
+                            for (int s = 1; s < kWaveSize; s <<= 1)
+                                pr ^= __shfl_xor(pr, s, kWaveSize);
+                            const uint32_t tn = __builtin_amdgcn_readlane(r.nmeta, j);
+                            const uint32_t tr = __builtin_amdgcn_readlane(r.raw, j);
+                            const uint32_t sn = tn - pn;   // suffix metadata bytes
+                            const uint32_t sr = tr ^ mulmod_horner(pr, xpow8_dev(sn));
+                            xexit = __builtin_amdgcn_readlane(r.exit, j);
+                            xcount = wc + gc - uint32_t(cut);
+                            xflags = fl;
+                            const uint32_t nn = wn + sn;
+                            const uint32_t rr = mulmod_horner(wr, xpow8_dev(sn)) ^ sr;
+                            if (lane == int(j)) {
+                                r.start = pos;
+                                r.count = xcount;
+                                r.nmeta = nn;
+                                r.raw = rr;
+                                r.pre = wc;
+                                r.cut = uint32_t(cut);
+                            }
+                        } else {
+                            // walked the whole part: C walks it once more
+                            xexit = p;
+                            xcount = wc;
+                            xflags = wflags;
+                            if (lane == int(j)) {
+                                r.start = pos;
+                                r.exit = p;
+                                r.count = wc;
+                                r.nmeta = wn;
+                                r.raw = wr;
+                                r.flags = wflags | kPartChase;
+                            }
+                        }
+                        have = true;
                     }
                 }
                 if (!have) {
@@ -2767,7 +2787,7 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
 // accepted as walked (the common case) already has its records in the
 // scratch A wrote: the wave copies them, part after part, 64 records per
 // instruction.  Entries walked by k_walk_fix before it met the guessed chain
-// are walked once more here (at most kMeet); parts walked again, or with more
+// are walked once more here; parts walked again in full, or with more
 // records than the scratch holds, are walked again here in full.
 __global__ __launch_bounds__(256) void k_walk_emit(PWalk w)
 {
