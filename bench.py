@@ -887,10 +887,19 @@ def main():
         log(f"bench: --gpus {n} but the launcher started WORLD_SIZE={env_world} ranks")
         return 2
 
+    # stdout carries exactly one JSON line: everything else the ranks' libraries
+    # print there (RCCL's version banner at communicator creation) goes to stderr
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
+
+    def emit(line):
+        os.write(json_fd, (json.dumps(line) + "\n").encode())
+
     from ramcloud_amd import ramcrc
     ramcrc.lib()  # fail loudly if the HIP library is missing
     if args.config == "host":
-        print(json.dumps(run_host()), flush=True)
+        emit(run_host())
         return 0
     if args.host_dry_run:
         ranks = Ranks("gloo")
@@ -907,7 +916,7 @@ def main():
                "replay": run_replay, "append": run_append, "stream": run_stream}[config]
         line = run(args, ranks)
     if ranks.rank == 0:
-        print(json.dumps(line), flush=True)
+        emit(line)
     ranks.close()
     return 0
 

@@ -721,7 +721,10 @@ __global__ __launch_bounds__(256) void k_combine(BatchDesc d, Plan pl, uint64_t 
 constexpr int kG = 8;                      // lanes per entry group
 constexpr uint64_t kStep = kG * 16;        // bytes per group step
 constexpr int kNB = 161;                   // step-count bins
-constexpr int kSmallK = 4;                 // bins 2..kSmallK: octets loaded one ahead
+#ifndef RAMCRC_SMALLK
+#define RAMCRC_SMALLK 4
+#endif
+constexpr int kSmallK = RAMCRC_SMALLK;     // bins 2..kSmallK: octets loaded one ahead
 constexpr int kPU = 4;                     // ping-pong depth (pipelined bins)
 constexpr uint32_t kNoIdx = 0xFFFFFFFFu;   // empty slot
 constexpr uint64_t kOctetCost = 4;         // per-octet overhead in step units (work split)
