@@ -69,7 +69,13 @@ VARIANTS = {
     "u4_c19": ["RAMCRC_UNROLL=4", "RAMCRC_CHUNK_SHIFT=19"],
     "u4_c17": ["RAMCRC_UNROLL=4", "RAMCRC_CHUNK_SHIFT=17"],
     "u4_c20": ["RAMCRC_UNROLL=4", "RAMCRC_CHUNK_SHIFT=20"],
-
+    # parallel-walk sync search (k_walk_sync)
+    "sh4": ["RAMCRC_SYNC_HOPS=4"],
+    "sh5": ["RAMCRC_SYNC_HOPS=5"],
+    "sp16": ["RAMCRC_SYNC_PER=16"],
+    "sp4": ["RAMCRC_SYNC_PER=4"],
+    "ss6": ["RAMCRC_SYNC_STAGE_KIB=6"],
+    "ss16": ["RAMCRC_SYNC_STAGE_KIB=16"],
 }
 
 

@@ -2070,9 +2070,19 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
 constexpr uint32_t kPartShift = 16;                 // 64 KiB parts
 constexpr uint32_t kPartBytes = 1u << kPartShift;
 constexpr uint32_t kNoStart = 0xFFFFFFFFu;
-constexpr int kSyncHops = 6;                        // hops a guess must survive
-constexpr int kSyncPer = 8;                         // candidates per lane per round
+#ifndef RAMCRC_SYNC_HOPS
+#define RAMCRC_SYNC_HOPS 6
+#endif
+#ifndef RAMCRC_SYNC_PER
+#define RAMCRC_SYNC_PER 8
+#endif
+#ifndef RAMCRC_SYNC_STAGE_KIB
+#define RAMCRC_SYNC_STAGE_KIB 9
+#endif
+constexpr int kSyncHops = RAMCRC_SYNC_HOPS;         // hops a guess must survive
+constexpr int kSyncPer = RAMCRC_SYNC_PER;           // candidates per lane per round
 constexpr uint32_t kSyncRound = kSyncPer * kWaveSize;   // 512 candidates
+static_assert(kSyncPer % 4 == 0 && kSyncPer <= 32, "candidates per lane: whole dwords");
 constexpr uint32_t kSyncSpan = 16384;               // candidate bytes searched per part
 constexpr uint32_t kRewalkBudget = 1u << 15;        // hops B may re-walk before falling back
 constexpr uint32_t kNumTypes = 12;                  // TOTAL_LOG_ENTRY_TYPES, src/LogEntryTypes.h:68
@@ -2177,7 +2187,7 @@ __device__ __forceinline__ uint32_t walk_limit(const PWalk& w, uint64_t seg)
 // A0: one wave per part k >= 1.  The part's first kSyncWin bytes are staged
 // in LDS, so most candidate hops (the true chain's included, for entries of
 // a few KiB) read LDS instead of waiting on global memory.
-constexpr uint32_t kSyncStage = 9216;                // staged bytes per wave (9 x 1 KiB)
+constexpr uint32_t kSyncStage = RAMCRC_SYNC_STAGE_KIB * 1024;   // staged bytes per wave
 constexpr uint32_t kSyncWin = kSyncStage - 16;       // candidates / hops read from LDS below this
 constexpr int kSyncWaves = 4;                        // waves per workgroup
 
@@ -2193,12 +2203,46 @@ __device__ __forceinline__ bool plausible(uint64_t q, const Hop& h, uint32_t cap
     return type != 0 && type < kNumTypes && canon && h.next <= capacity;
 }
 
+// First-hop filter of four candidates at once (bytes of h, one candidate
+// per byte; top3 = for each, the byte three further on, the top length byte
+// of a 3-byte length): a superset of plausible() -- the type is 1..11, and,
+// where the capacity rules them out, no 4-byte length (>= 2^24 when
+// canonical) and no 3-byte length with its top bit set (>= 2^23).  Returns
+// one bit per candidate.
+__device__ __forceinline__ uint32_t first_hop4(uint32_t h, uint32_t top3, bool kill4, bool kill3)
+{
+    const uint32_t t = h & 0x3f3f3f3fu;
+    constexpr uint32_t kLo = 0x3f3f3f3fu;                      // t + 63 >= 64 iff t >= 1
+    constexpr uint32_t kHi = 0x01010101u * (64 - kNumTypes);    // t + 52 >= 64 iff t >= 12
+    uint32_t ok = ((t + kLo) & ~(t + kHi) & 0x40404040u) << 1;   // bit 7 of each byte
+    const uint32_t lb4 = h & (h << 1) & 0x80808080u;
+    const uint32_t lb3 = h & ~(h << 1) & 0x80808080u;
+    ok &= ~((kill4 ? lb4 : 0u) | (kill3 ? (lb3 & top3) : 0u));
+    const uint32_t x = ok >> 7;
+    return (x | (x >> 7) | (x >> 14) | (x >> 21)) & 0xFu;
+}
+
+// Wave minimum through DPP (quad swaps, half-row and row mirrors, row
+// broadcasts): the result is valid in lane 63 and returned uniform.
+__device__ __forceinline__ uint32_t wave_min(uint32_t v)
+{
+    v = min(v, uint32_t(__builtin_amdgcn_update_dpp(-1, int(v), 0xB1, 0xF, 0xF, false)));   // quad_perm 1,0,3,2
+    v = min(v, uint32_t(__builtin_amdgcn_update_dpp(-1, int(v), 0x4E, 0xF, 0xF, false)));   // quad_perm 2,3,0,1
+    v = min(v, uint32_t(__builtin_amdgcn_update_dpp(-1, int(v), 0x141, 0xF, 0xF, false)));  // row_half_mirror
+    v = min(v, uint32_t(__builtin_amdgcn_update_dpp(-1, int(v), 0x140, 0xF, 0xF, false)));  // row_mirror
+    v = min(v, uint32_t(__builtin_amdgcn_update_dpp(-1, int(v), 0x142, 0xA, 0xF, false)));  // row_bcast:15
+    v = min(v, uint32_t(__builtin_amdgcn_update_dpp(-1, int(v), 0x143, 0xC, 0xF, false)));  // row_bcast:31
+    return uint32_t(__builtin_amdgcn_readlane(int(v), 63));
+}
+
 __global__ __launch_bounds__(kSyncWaves * kWaveSize) void k_walk_sync(PWalk w)
 {
     __shared__ __attribute__((aligned(16))) uint8_t wins[kSyncWaves][kSyncStage];
+    __shared__ uint16_t lists[kSyncWaves][kSyncRound];   // a round's first-hop survivors
     const int lane = threadIdx.x & (kWaveSize - 1);
     const int wv = threadIdx.x / kWaveSize;
     uint8_t* win = wins[wv];
+    uint16_t* list = lists[wv];
     const uint64_t nwave = uint64_t(gridDim.x) * kSyncWaves;
     const uint64_t total = w.nseg * w.nparts;
     for (uint64_t i = uint64_t(blockIdx.x) * kSyncWaves + wv; i < total; i += nwave) {
@@ -2253,69 +2297,51 @@ __global__ __launch_bounds__(kSyncWaves * kWaveSize) void k_walk_sync(PWalk w)
         // hops).  h lies below the first hop of every survivor (a survivor
         // before h jumps over it, h itself hops to the next real header), so
         // the scan stops at the nearest first hop seen.
-        // Per round: lane l tests candidates c0 + 8 l + j (j < 8) on its
-        // first hop from three words it holds; the ~10 % that pass are
-        // compacted, one per lane, and chased level by level -- one peek per
-        // lane per level instead of a loop over eight slots.  LDS-only: a hop
+        // Per round: lane l filters candidates c0 + 8 l + j (j < 8) four at a
+        // time with byte-parallel (SWAR) tests on the words it holds
+        // (first_hop4); the ~10 % that pass are listed in LDS and chased one
+        // per lane, level by level (level 0 is the exact plausible() test),
+        // and the wave minima are DPP reductions.  LDS-only: a hop
         // that leaves the staged window ends the candidate (no global round
         // trip for any lane); otherwise beyond-window hops read global memory.
+        const bool kill4 = w.capacity <= (1u << 24);   // a 4-byte length ends past it
+        const bool kill3 = w.capacity <= (1u << 23);   // so does a 3-byte one >= 2^23
         auto search = [&](bool lds_only, uint32_t to) -> uint32_t {
             const uint32_t wend = B + kSyncWin;   // peeks below wend stay in LDS
             uint64_t best = ~0ull;                // (position after two hops << 32) | candidate
             uint32_t bound = 0xFFFFFFFFu;         // nearest first hop of a survivor: h lies below it
             for (uint32_t c0 = B; c0 < to && c0 < bound; c0 += kSyncRound) {
                 const uint32_t cl = c0 + uint32_t(lane) * kSyncPer;
-                uint32_t d0, d1, d2;
-                {
-                    const uint64_t lo = peek(cl), hi = peek(cl + 4), hi2 = peek(cl + 8);
-                    d0 = uint32_t(lo);
-                    d1 = uint32_t(hi);
-                    d2 = uint32_t(hi2);
+                constexpr int kWords = (kSyncPer / 4 + 3) & ~1;
+                uint32_t d[kWords];   // bytes [cl, cl + kSyncPer + 8) and up to 4 more
+#pragma unroll
+                for (int u = 0; u < kWords; u += 2) {
+                    const uint64_t v = peek(cl + 4 * u);
+                    d[u] = uint32_t(v);
+                    d[u + 1] = uint32_t(v >> 32);
                 }
                 uint32_t alive = 0;
 #pragma unroll
-                for (int j = 0; j < kSyncPer; j++) {
-                    const uint32_t c = cl + j;
-                    const uint64_t w01 = (uint64_t(d1) << 32) | d0, w12 = (uint64_t(d2) << 32) | d1;
-                    const uint64_t q = (j < 4 ? w01 : w12) >> (8 * (j & 3));
-                    const Hop h = hop_of(q, c);
-                    alive |= (c < to && plausible(q, h, w.capacity)) ? (1u << j) : 0u;
-                }
-                // survivors, slot-major: mask[j] bit l = candidate c0 + 8 l + j
-                uint32_t cnt[kSyncPer];
-                uint64_t mask[kSyncPer];
+                for (int g = 0; g < kSyncPer / 4; g++)
+                    alive |= first_hop4(d[g], __builtin_amdgcn_alignbyte(d[g + 1], d[g], 3), kill4,
+                                        kill3)
+                             << (4 * g);
+                alive &= to > cl ? (to - cl >= kSyncPer ? ~0u : (1u << (to - cl)) - 1u) : 0u;
+                // survivors listed slot-major in LDS (offsets from c0)
                 uint32_t total = 0;
 #pragma unroll
                 for (int j = 0; j < kSyncPer; j++) {
-                    mask[j] = __ballot((alive >> j) & 1);
-                    cnt[j] = uint32_t(__popcll(mask[j]));
-                    total += cnt[j];
+                    const uint64_t m = __ballot((alive >> j) & 1);
+                    const uint32_t at = total + __builtin_amdgcn_mbcnt_hi(
+                                                    uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+                    if ((alive >> j) & 1)
+                        list[at] = uint16_t(uint32_t(lane) * kSyncPer + j);
+                    total += uint32_t(__popcll(m));
                 }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 for (uint32_t t0 = 0; t0 < total; t0 += kWaveSize) {
-                    // lane -> its survivor: slot j, then the n-th set bit of mask[j]
-                    uint32_t n = t0 + uint32_t(lane);
-                    const bool have = n < total;
-                    uint64_t m = 0;
-                    uint32_t jj = 0;
-#pragma unroll
-                    for (int j = 0; j < kSyncPer; j++) {
-                        const bool here = have && m == 0 && n < cnt[j];
-                        m = here ? mask[j] : m;
-                        jj = here ? uint32_t(j) : jj;
-                        n = (have && !here && m == 0) ? n - cnt[j] : n;
-                    }
-                    // n-th (0-based) set bit of m by halving
-                    uint32_t pos = 0;
-#pragma unroll
-                    for (int width = 32; width >= 1; width >>= 1) {
-                        const uint64_t lowmask = width == 64 ? ~0ull : ((1ull << width) - 1);
-                        const uint32_t c = uint32_t(__popcll((m >> pos) & lowmask));
-                        if (n >= c) {
-                            n -= c;
-                            pos += width;
-                        }
-                    }
-                    uint32_t c = cl - uint32_t(lane) * kSyncPer + pos * kSyncPer + jj;   // c0 + 8 pos + jj
+                    const bool have = t0 + uint32_t(lane) < total;
+                    const uint32_t c = c0 + (have ? list[t0 + uint32_t(lane)] : 0u);
                     bool live = have;
                     uint32_t p = c, first = 0, second = 0;
                     for (int hh = 0; hh < kSyncHops && __ballot(live && p < limit); hh++) {
@@ -2340,20 +2366,18 @@ __global__ __launch_bounds__(kSyncWaves * kWaveSize) void k_walk_sync(PWalk w)
                         second = p;
                     if (first == 0)
                         first = p;
-                    uint64_t key = live ? ((uint64_t(second) << 32) | c) : ~0ull;
-                    uint32_t fb = live ? first : 0xFFFFFFFFu;
-#pragma unroll
-                    for (int s = 1; s < kWaveSize; s <<= 1)
-                        fb = min(fb, uint32_t(__shfl_xor(fb, s, kWaveSize)));
+                    const uint32_t fb = wave_min(live ? first : 0xFFFFFFFFu);
                     bound = fb < bound ? fb : bound;
-#pragma unroll
-                    for (int s = 1; s < kWaveSize; s <<= 1) {
-                        const uint32_t lo = __shfl_xor(uint32_t(key), s, kWaveSize);
-                        const uint32_t hi = __shfl_xor(uint32_t(key >> 32), s, kWaveSize);
-                        const uint64_t o = (uint64_t(hi) << 32) | lo;
-                        key = o < key ? o : key;
+                    // nearest second hop, ties to the lower candidate
+                    const uint32_t s2 = wave_min(live ? second : 0xFFFFFFFFu);
+                    if (s2 != 0xFFFFFFFFu) {
+                        const uint64_t tie = __ballot(live && second == s2);
+                        const uint32_t lo = __popcll(tie) == 1
+                                                ? uint32_t(__builtin_amdgcn_readlane(int(c), __builtin_ctzll(tie)))
+                                                : wave_min(live && second == s2 ? c : 0xFFFFFFFFu);
+                        const uint64_t key = (uint64_t(s2) << 32) | lo;
+                        best = key < best ? key : best;
                     }
-                    best = key < best ? key : best;
                 }
             }
             return best == ~0ull ? kNoStart : uint32_t(best);
