@@ -76,6 +76,14 @@ VARIANTS = {
     "sp4": ["RAMCRC_SYNC_PER=4"],
     "ss6": ["RAMCRC_SYNC_STAGE_KIB=6"],
     "ss16": ["RAMCRC_SYNC_STAGE_KIB=16"],
+    "ss8": ["RAMCRC_SYNC_STAGE_KIB=8"],
+    "ss12": ["RAMCRC_SYNC_STAGE_KIB=12"],
+    "ps15": ["RAMCRC_PART_SHIFT=15"],
+    "ps17": ["RAMCRC_PART_SHIFT=17"],
+    "tv1": ["RAMCRC_TINY_V=1"],
+    # k_entries ping-pong depth / waves per CU
+    "pu4": ["RAMCRC_PU=4"],
+    "ew8": ["RAMCRC_ENT_WAVES=8"],
 }
 
 

@@ -724,8 +724,21 @@ constexpr int kNB = 161;                   // step-count bins
 #ifndef RAMCRC_SMALLK
 #define RAMCRC_SMALLK 4
 #endif
+#ifndef RAMCRC_TINY_V
+#define RAMCRC_TINY_V 0   // 1: the unpipelined k_entries_tiny (A/B reference)
+#endif
+#ifndef RAMCRC_ENT_WAVES
+#define RAMCRC_ENT_WAVES 16
+#endif
+constexpr int kEntWaves = RAMCRC_ENT_WAVES;   // k_entries: waves per workgroup (1 per CU)
 constexpr int kSmallK = RAMCRC_SMALLK;     // bins 2..kSmallK: octets loaded one ahead
-constexpr int kPU = 4;                     // ping-pong depth (pipelined bins)
+#ifndef RAMCRC_ENT_NT
+#define RAMCRC_ENT_NT 1
+#endif
+#ifndef RAMCRC_PU
+#define RAMCRC_PU 2   // A/B on the config-3 mix, 1 KiB and 4 KiB entries: 2 < 1, 3, 4, 6, 8
+#endif
+constexpr int kPU = RAMCRC_PU;             // ping-pong depth (pipelined bins)
 constexpr uint32_t kNoIdx = 0xFFFFFFFFu;   // empty slot
 constexpr uint64_t kOctetCost = 4;         // per-octet overhead in step units (work split)
 constexpr int kBinPer = 4;                 // entries per thread per tile (count/scatter)
@@ -1131,6 +1144,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_entries_tiny(BatchDesc d, Sorte
                 const uint32_t i2 = tab[ib - 512 + ((in >> 16) & 0xFF)], i3 = tab[ib - 768 + (in >> 24)];
                 // one wait for all 20 lookups, then a 3-input XOR tree
                 const uint32_t ri = gl == 0 ? xor3(i0, i1, i2) ^ i3 : 0u;
+
                 const uint32_t t0 = xor3(v[0], v[1], v[2]), t1 = xor3(v[3], v[4], v[5]);
                 const uint32_t t2 = xor3(v[6], v[7], v[8]), t3 = xor3(v[9], v[10], v[11]);
                 const uint32_t t4 = xor3(v[12], v[13], v[14]), t5 = xor3(v[15], ri, t0);
@@ -1146,6 +1160,149 @@ __global__ __launch_bounds__(kThreads, 1) void k_entries_tiny(BatchDesc d, Sorte
             R = group8_xor(R);
             if (gl == 0 && ix[q] != kNoIdx)
                 d.out[ix[q]] = finalize ? ~R : R;
+        }
+    }
+}
+
+// Pipelined form of k_entries_tiny.  Round r of a wave covers 64 sorted
+// slots; lane L owns slot 64 r + L: it loads that descriptor (one coalesced
+// 1 KiB load per round instead of eight group-redundant ones), and at the end
+// folds in the slot's initial state and stores its result.  Group g hashes
+// the entries of lanes 8 g .. 8 g + 7 in turn, reading each owner's window
+// (base, offset, length) by swizzle within the group.  Descriptors are loaded
+// two rounds ahead and data one round ahead, so a wave's rounds overlap their
+// memory latency with the previous round's lookups.
+struct TinyOwn {
+    uint64_t S, A;        // entry start; its 16-byte piece
+    uint32_t geo;         // len (bits 0-7) | (S - A) << 8 for len >= 4 in bin 1; else 0
+    uint32_t len, ix, init;
+};
+
+template <int q>
+__device__ __forceinline__ uint32_t swz_from(uint32_t v)
+{
+    // lane (lane & 0x18) | q within each 32-lane half: lane q of this group
+    return uint32_t(__builtin_amdgcn_ds_swizzle(int(v), 0x18 | (q << 5)));
+}
+
+template <int q = 0, class F>
+__device__ __forceinline__ void static_for8(F&& f)
+{
+    if constexpr (q < 8) {
+        f(std::integral_constant<int, q>{});
+        static_for8<q + 1>(f);
+    }
+}
+
+__global__ __launch_bounds__(kThreads, 1) void k_entries_tiny_pipe(BatchDesc d, Sorted so)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsTiny];
+    if (so.bt->start[2] == so.bt->start[0])
+        return;   // no entry of at most one window (uniform: every wave exits)
+    const int lane = threadIdx.x & (kWaveSize - 1);
+    const int gl = lane & 7;
+    const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerGroup +
+                          __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
+    const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerGroup;
+    const uint64_t s0 = so.bt->start[0], s1 = so.bt->start[2];
+    const uint64_t rounds = (s1 - s0 + 63) / 64;
+    const bool finalize = d.flags & RAMCRC_FINALIZE;
+    const uint64_t dummy = reinterpret_cast<uint64_t>(so.bt);
+
+    auto load_own = [&](uint64_t r) -> TinyOwn {
+        TinyOwn o;
+        const uint64_t sl = s0 + r * 64 + uint32_t(lane);
+        u32x4 dd = {0u, 0u, 0u, 0u};
+        o.ix = kNoIdx;
+        o.init = 0xFFFFFFFFu;
+        if (r < rounds && sl < s1) {
+            dd = so.desc[sl];
+            o.ix = so.idx[sl];
+            if (d.init)
+                o.init = so.init[sl];
+        }
+        o.S = (uint64_t(dd.y) << 32) | dd.x;
+        const uint64_t E = (uint64_t(dd.w) << 32) | dd.z;
+        o.len = uint32_t(E - o.S);
+        o.A = o.S & ~uint64_t(15);
+        o.geo = (o.ix != kNoIdx && o.len >= 4) ? (o.len | (uint32_t(o.S - o.A) << 8)) : 0u;
+        return o;
+    };
+    // the group's eight windows: piece gl of each owner's 128-byte window
+    auto issue = [&](const TinyOwn& o, u32x4 (&w)[8], uint32_t (&geo)[8]) {
+        static_for8([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            geo[q] = swz_from<q>(o.geo);
+            const uint64_t A = (uint64_t(swz_from<q>(uint32_t(o.A >> 32))) << 32) |
+                               swz_from<q>(uint32_t(o.A));
+            const uint32_t e = ((geo[q] >> 8) & 0xF) + (geo[q] & 0xFF);   // E - A
+            const bool ok = geo[q] != 0 && uint32_t(gl) * 16 < e;
+            w[q] = load16(ok ? A + uint32_t(gl) * 16 : (geo[q] ? A : dummy));   // past E: zero rows
+        });
+    };
+
+    uint64_t r = wave;
+    TinyOwn o0 = load_own(r), o1 = load_own(r + nwaves);
+    fill_plain(lds, 0, &g_tab.pos[0][0], 132 * 256);
+    __syncthreads();
+    const uint32_t* tab = reinterpret_cast<const uint32_t*>(lds);
+    u32x4 wc[8];
+    uint32_t gc[8];
+    issue(o0, wc, gc);
+    for (; r < rounds; r += nwaves) {
+        const TinyOwn o2 = load_own(r + 2 * nwaves);
+        u32x4 wn[8];
+        uint32_t gn[8];
+        if (r + nwaves < rounds)
+            issue(o1, wn, gn);
+        uint32_t mine = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const uint32_t len = gc[q] & 0xFF;
+            const int sa = int((gc[q] >> 8) & 0xF);
+            const int ds = sa - 16 * gl;                 // S - a
+            const int e = sa + int(len) - 16 * gl;       // E - a (<= 128)
+            const uint32_t ws[4] = {wc[q].x, wc[q].y, wc[q].z, wc[q].w};
+            uint32_t v[16];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t x = ws[j] & ~keep_lo(ds - 4 * j);
+                const uint32_t base = uint32_t(max(e - 4 * j, 0)) << 8;
+#pragma unroll
+                for (int t = 0; t < 4; t++)
+                    v[4 * j + t] = tab[base + ((x >> (8 * t)) & 0xFF) + (kTinyRow0 - t) * 256];
+            }
+            const uint32_t t0 = xor3(v[0], v[1], v[2]), t1 = xor3(v[3], v[4], v[5]);
+            const uint32_t t2 = xor3(v[6], v[7], v[8]), t3 = xor3(v[9], v[10], v[11]);
+            const uint32_t t4 = xor3(v[12], v[13], v[14]);
+            uint32_t R = xor3(xor3(t0, t1, t2), xor3(t3, t4, v[15]), 0u);
+            R ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(R), 0xB1, 0xF, 0xF, false));   // lane ^ 1
+            R ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(R), 0x4E, 0xF, 0xF, false));   // lane ^ 2
+            R ^= uint32_t(__builtin_amdgcn_ds_swizzle(int(R), 0x1F | (4 << 10)));           // lane ^ 4
+            mine = gl == q ? R : mine;
+        }
+        // own slot: the initial state (byte k at distance len - k), or bytewise
+        if (o0.ix != kNoIdx) {
+            uint32_t R;
+            if (o0.len >= 4) {
+                const uint32_t ib = (o0.len + kTinyRow0) << 8;
+                const uint32_t in = o0.init;
+                R = mine ^ xor3(tab[ib + (in & 0xFF)], tab[ib - 256 + ((in >> 8) & 0xFF)],
+                                tab[ib - 512 + ((in >> 16) & 0xFF)]) ^
+                    tab[ib - 768 + (in >> 24)];
+            } else {
+                R = o0.init;
+                for (uint32_t k = 0; k < o0.len; k++)
+                    R = tab[(1 + kTinyRow0) * 256 + ((R ^ *(const gu8*)(o0.S + k)) & 0xFF)] ^ (R >> 8);
+            }
+            d.out[o0.ix] = finalize ? ~R : R;
+        }
+        o0 = o1;
+        o1 = o2;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            wc[q] = wn[q];
+            gc[q] = gn[q];
         }
     }
 }
@@ -1180,9 +1337,9 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
     const int lane = threadIdx.x & (kWaveSize - 1);
     const int g = lane >> 3, gl = lane & 7;
     const RepOp op(lane);
-    const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerGroup +
+    const uint64_t wave = uint64_t(blockIdx.x) * kEntWaves +
                           __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
-    const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerGroup;
+    const uint64_t nwaves = uint64_t(gridDim.x) * kEntWaves;
     const uint64_t I0 = s_items[b0], T = s_items[b1] - I0;
     const uint64_t lo = I0 + T * wave / nwaves, hi = I0 + T * (wave + 1) / nwaves;
     const bool finalize = d.flags & RAMCRC_FINALIZE;
@@ -1339,7 +1496,11 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
             // loads: head, first two tail steps, first kPU interior steps
             const gu32x4* pb = gptr16(steps ? p0 : dummy);
             const uint64_t bstride = steps ? kStep / 16 : 0;
+#if RAMCRC_ENT_NT
             auto ldf = [&](uint64_t k) -> u32x4 { return __builtin_nontemporal_load(pb + k * bstride); };
+#else
+            auto ldf = [&](uint64_t k) -> u32x4 { return pb[k * bstride]; };
+#endif
             auto ldt = [&](uint32_t k) -> u32x4 {   // tail step: lanes past E read a safe word
                 const uint64_t a = p0 + uint64_t(k) * kStep;
                 return load16(k < steps && a < E ? a : safe);
@@ -1443,7 +1604,7 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
 // Both phases in one launch (one LDS fill, one launch boundary): the exact
 // short bins, then the pipelined long bins.  The phases are separate inlined
 // loops, so the long-entry loop's registers are not shared with the short one.
-__global__ __launch_bounds__(kThreads, 1) void k_entries(BatchDesc d, Sorted so)
+__global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc d, Sorted so)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsEntries];
     if (so.bt->items[2] == so.bt->items[kNB])
@@ -1746,8 +1907,12 @@ int launch_binned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_lar
     HIPCHK(hipGetLastError());
     {
         ScanTimer t(c, s);
+#if RAMCRC_TINY_V == 0
+        hipLaunchKernelGGL(k_entries_tiny_pipe, dim3(c->ncu), dim3(kThreads), 0, s, d, so);
+#else
         hipLaunchKernelGGL(k_entries_tiny, dim3(c->ncu), dim3(kThreads), 0, s, d, so);
-        hipLaunchKernelGGL(k_entries, dim3(c->ncu), dim3(kThreads), 0, s, d, so);
+#endif
+        hipLaunchKernelGGL(k_entries, dim3(c->ncu), dim3(kEntWaves * kWaveSize), 0, s, d, so);
     }
     HIPCHK(hipGetLastError());
     return RAMCRC_OK;
@@ -2067,7 +2232,10 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
 // serial walker k_seg_walk, which implements those semantics.  The result of
 // every segment -- flags, checksum, entry count, records -- equals the serial
 // walk's (tests/test_gpu_segments.py runs both against the oracle).
-constexpr uint32_t kPartShift = 16;                 // 64 KiB parts
+#ifndef RAMCRC_PART_SHIFT
+#define RAMCRC_PART_SHIFT 16
+#endif
+constexpr uint32_t kPartShift = RAMCRC_PART_SHIFT;  // 64 KiB parts
 constexpr uint32_t kPartBytes = 1u << kPartShift;
 constexpr uint32_t kNoStart = 0xFFFFFFFFu;
 #ifndef RAMCRC_SYNC_HOPS
