@@ -542,8 +542,8 @@ def run_entries(args, ranks):
                    "path": args.path,
                    "parallelism": f"replicas{ranks.world}" if ranks.world > 1 else "single",
                    "exchange": "none", "table_bytes_not_credited": 16 * lens.size},
-        "roofline": dict(roofline("k_entries_tiny+k_entries" if args.path == "entries"
-                                  else "k_chunks+k_entries_tiny+k_entries", total, scan_ms, key),
+        "roofline": dict(roofline("k_entries (tiny + long phases)" if args.path == "entries"
+                                  else "k_chunks+k_entries", total, scan_ms, key),
                          scan_ms_per_step=round(scan_ms, 4)),
         "cpu_baseline": cpu,
     }

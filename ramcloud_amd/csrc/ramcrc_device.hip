@@ -85,7 +85,7 @@ struct alignas(16) DeviceTables {
     ramcrc::ByteTable t0;   // X^1 byte step
     uint32_t xblk[4][256];  // x^(8 * 1024 * b * 256^j)
     uint32_t xinv[1024];    // x^(-8 p)
-    uint32_t pos[132][256]; // k_entries_tiny: row r = X^(r-3)(byte), rows 0..3 (m <= 0) zero
+    uint32_t pos[132][256]; // k_entries, tiny phase: row r = X^(r-3)(byte), rows 0..3 (m <= 0) zero
     uint32_t xmeta[5 * 64 + 1];   // k_seg_walk: x^(8d), d = 0 .. 320 (one batch of metadata)
     uint32_t xbyte[4][256];       // x^(8 * b * 256^j): x^(8d) for any 32-bit d in 4 factors
 };
@@ -724,9 +724,6 @@ constexpr int kNB = 161;                   // step-count bins
 #ifndef RAMCRC_SMALLK
 #define RAMCRC_SMALLK 4
 #endif
-#ifndef RAMCRC_TINY_V
-#define RAMCRC_TINY_V 0   // 1: the unpipelined k_entries_tiny (A/B reference)
-#endif
 #ifndef RAMCRC_ENT_WAVES
 #define RAMCRC_ENT_WAVES 16
 #endif
@@ -743,8 +740,9 @@ constexpr uint32_t kNoIdx = 0xFFFFFFFFu;   // empty slot
 constexpr uint64_t kOctetCost = 4;         // per-octet overhead in step units (work split)
 constexpr int kBinPer = 4;                 // entries per thread per tile (count/scatter)
 
-constexpr uint32_t kTinyRow0 = 3;            // k_entries_tiny: row of distance m is m + 3
-constexpr uint32_t kLdsTiny = 132 * 1024;    // k_entries_tiny: X^m(byte), m = -3..128
+constexpr uint32_t kTinyRow0 = 3;            // tiny phase: row of distance m is m + 3
+constexpr uint32_t kLdsTiny = 132 * 1024;    // tiny phase: X^m(byte), m = -3..128
+static_assert(kLdsTiny <= kLdsEntries, "k_entries' LDS holds the tiny phase's table");
 
 struct BinTable {
     uint64_t start[kNB];      // first sorted slot of the bin (multiple of 8)
@@ -1069,102 +1067,7 @@ __device__ __forceinline__ uint32_t group8_xor(uint32_t v)
 // here): no Horner step and no per-entry multiply.  Byte b at distance m from
 // the entry end contributes X^m(b), read from a 132 x 256 LDS table (rows for
 // m <= 0 are zero), so a lane does 16 lookups for its 16 bytes and the group
-// XORs its 8 lanes.  Every lane reads its group's descriptor itself (8 lanes,
-// one address: no cross-lane shuffles), and eight octets share one load round.
-__global__ __launch_bounds__(kThreads, 1) void k_entries_tiny(BatchDesc d, Sorted so)
-{
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsTiny];
-    if (so.bt->start[2] == so.bt->start[0])
-        return;   // no entry of at most one window (uniform: every wave exits)
-    fill_plain(lds, 0, &g_tab.pos[0][0], 132 * 256);
-    __syncthreads();
-    const uint32_t* tab = reinterpret_cast<const uint32_t*>(lds);
-
-    const int lane = threadIdx.x & (kWaveSize - 1);
-    const int g = lane >> 3, gl = lane & 7;
-    const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerGroup +
-                          __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
-    const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerGroup;
-    const uint64_t s0 = so.bt->start[0], s1 = so.bt->start[2];
-    const uint64_t rounds = (s1 - s0 + 63) / 64;
-    const bool finalize = d.flags & RAMCRC_FINALIZE;
-    const uint64_t dummy = reinterpret_cast<uint64_t>(so.bt);
-
-    for (uint64_t r = wave; r < rounds; r += nwaves) {
-        uint32_t geo[8], ix[8], init[8];
-        u32x4 w[8];
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const uint64_t slot = s0 + r * 64 + q * kG + g;
-            u32x4 dd = {0u, 0u, 0u, 0u};
-            ix[q] = kNoIdx;
-            init[q] = 0xFFFFFFFFu;
-            if (slot < s1) {
-                dd = so.desc[slot];
-                ix[q] = so.idx[slot];
-                if (d.init)
-                    init[q] = so.init[slot];
-            }
-            const uint64_t S = (uint64_t(dd.y) << 32) | dd.x;
-            const uint64_t E = (uint64_t(dd.w) << 32) | dd.z;
-            const uint64_t A = S & ~uint64_t(15);
-            const uint64_t a = A + gl * 16;
-            // geo: len (bits 0-7, <= 128), S - a + 128 (8-15), E - a + 128 (16-24: up
-            // to 256, when the entry ends exactly at the end of its window)
-            geo[q] = uint32_t(E - S) | (uint32_t(int(int64_t(S - a)) + 128) << 8) |
-                     (uint32_t(int(int64_t(E - a)) + 128) << 16);
-            const bool big = E - S >= 4;
-            const bool ok = big && a < E;
-            w[q] = load16(ok ? a : (big ? A : dummy));   // pieces past E hit zero rows
-        }
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const uint32_t len = geo[q] & 0xFF;
-            const int ds = int((geo[q] >> 8) & 0xFF) - 128;    // S - a (<= 15)
-            const int e = int((geo[q] >> 16) & 0x1FF) - 128;   // E - a (<= 128)
-            uint32_t R = 0;
-            if (len >= 4) {
-                // Byte at distance m from E contributes row m + 3; bytes at or
-                // past E (m <= 0) land in the zero rows, so only the bytes
-                // before S need a mask.  The init is not injected into the
-                // data: its byte k sits at distance len - k (4 more lookups).
-                const uint32_t ws[4] = {w[q].x, w[q].y, w[q].z, w[q].w};
-                uint32_t v[16];
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const uint32_t x = ws[j] & ~keep_lo(ds - 4 * j);
-                    const uint32_t base = uint32_t(max(e - 4 * j, 0)) << 8;   // row of byte 0, - 3
-#pragma unroll
-                    for (int t = 0; t < 4; t++)
-                        v[4 * j + t] = tab[base + ((x >> (8 * t)) & 0xFF) + (kTinyRow0 - t) * 256];
-                }
-                const uint32_t in = init[q];
-                const uint32_t ib = (len + kTinyRow0) << 8;
-                const uint32_t i0 = tab[ib + (in & 0xFF)], i1 = tab[ib - 256 + ((in >> 8) & 0xFF)];
-                const uint32_t i2 = tab[ib - 512 + ((in >> 16) & 0xFF)], i3 = tab[ib - 768 + (in >> 24)];
-                // one wait for all 20 lookups, then a 3-input XOR tree
-                const uint32_t ri = gl == 0 ? xor3(i0, i1, i2) ^ i3 : 0u;
-
-                const uint32_t t0 = xor3(v[0], v[1], v[2]), t1 = xor3(v[3], v[4], v[5]);
-                const uint32_t t2 = xor3(v[6], v[7], v[8]), t3 = xor3(v[9], v[10], v[11]);
-                const uint32_t t4 = xor3(v[12], v[13], v[14]), t5 = xor3(v[15], ri, t0);
-                R = xor3(xor3(t1, t2, t3), t4, t5);
-            } else if (gl == 0) {
-                // 0-3 bytes: byte steps from the initial state
-                R = init[q];
-                const u32x4 dd = so.desc[s0 + r * 64 + q * kG + g];   // rare: reload S
-                const uint64_t S = (uint64_t(dd.y) << 32) | dd.x;
-                for (uint32_t k = 0; k < len; k++)
-                    R = tab[(1 + kTinyRow0) * 256 + ((R ^ *(const gu8*)(S + k)) & 0xFF)] ^ (R >> 8);
-            }
-            R = group8_xor(R);
-            if (gl == 0 && ix[q] != kNoIdx)
-                d.out[ix[q]] = finalize ? ~R : R;
-        }
-    }
-}
-
-// Pipelined form of k_entries_tiny.  Round r of a wave covers 64 sorted
+// XORs its 8 lanes.  Round r of a wave covers 64 sorted
 // slots; lane L owns slot 64 r + L: it loads that descriptor (one coalesced
 // 1 KiB load per round instead of eight group-redundant ones), and at the end
 // folds in the slot's initial state and stores its result.  Group g hashes
@@ -1194,16 +1097,16 @@ __device__ __forceinline__ void static_for8(F&& f)
     }
 }
 
-__global__ __launch_bounds__(kThreads, 1) void k_entries_tiny_pipe(BatchDesc d, Sorted so)
+// The first phase of k_entries; lds holds the position table (kLdsTiny bytes).
+__device__ __forceinline__ void tiny_run(const BatchDesc& d, const Sorted& so, uint8_t* lds)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsTiny];
     if (so.bt->start[2] == so.bt->start[0])
         return;   // no entry of at most one window (uniform: every wave exits)
     const int lane = threadIdx.x & (kWaveSize - 1);
     const int gl = lane & 7;
-    const uint64_t wave = uint64_t(blockIdx.x) * kWavesPerGroup +
+    const uint64_t wave = uint64_t(blockIdx.x) * kEntWaves +
                           __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
-    const uint64_t nwaves = uint64_t(gridDim.x) * kWavesPerGroup;
+    const uint64_t nwaves = uint64_t(gridDim.x) * kEntWaves;
     const uint64_t s0 = so.bt->start[0], s1 = so.bt->start[2];
     const uint64_t rounds = (s1 - s0 + 63) / 64;
     const bool finalize = d.flags & RAMCRC_FINALIZE;
@@ -1607,8 +1510,10 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
 __global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc d, Sorted so)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsEntries];
+    tiny_run(d, so, lds);
     if (so.bt->items[2] == so.bt->items[kNB])
         return;   // every entry is tiny (or large on the batch path)
+    __syncthreads();   // the position table is dead: refill the LDS
     fill_replicated(lds, g_tab.stride_small);
     fill_plain(lds, kX4Off, &g_tab.comb[0].t[0][0], 4 * 1024);
     fill_plain(lds, kXinvOff, g_tab.xinv, 128);
@@ -1907,11 +1812,6 @@ int launch_binned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_lar
     HIPCHK(hipGetLastError());
     {
         ScanTimer t(c, s);
-#if RAMCRC_TINY_V == 0
-        hipLaunchKernelGGL(k_entries_tiny_pipe, dim3(c->ncu), dim3(kThreads), 0, s, d, so);
-#else
-        hipLaunchKernelGGL(k_entries_tiny, dim3(c->ncu), dim3(kThreads), 0, s, d, so);
-#endif
         hipLaunchKernelGGL(k_entries, dim3(c->ncu), dim3(kEntWaves * kWaveSize), 0, s, d, so);
     }
     HIPCHK(hipGetLastError());
