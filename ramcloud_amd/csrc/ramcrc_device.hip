@@ -748,7 +748,7 @@ struct BinTable {
     uint64_t start[kNB];      // first sorted slot of the bin (multiple of 8)
     uint64_t count[kNB];      // entries in the bin
     uint64_t items[kNB + 1];  // exclusive prefix of octets * kmax: work units
-    uint64_t cursor[kNB];     // scatter cursors
+    uint64_t cursor[kNB];     // scatter cursors, relative to start; zero between launches
     uint64_t kcost[kNB];      // steps charged per octet of the bin (observed max)
     uint32_t hist[kNB];       // entry counts; zero between launches
     uint32_t kobs[kNB];       // observed max steps (log-scale bins); zero between launches
@@ -865,66 +865,76 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
     }
 }
 
-__global__ __launch_bounds__(256) void k_bin_scan(Sorted so)
+// Bin layout from the histogram, computed by every k_bin_scatter workgroup
+// for itself (no separate scan launch): threads 0..255 take one bin each and
+// run parallel exclusive scans of the slot counts and of the work units.
+// Workgroup 0 also publishes the layout k_entries reads (start, items, kcost)
+// and empties the padding slots of each bin's last octet.  Every thread of
+// the block calls this (it synchronises).
+struct BinScratch {
+    uint64_t start[kNB], count[kNB];
+    uint64_t wpos[4], witem[4];
+};
+
+__device__ __forceinline__ void bin_layout(const Sorted& so, BinScratch& sc, bool publish)
 {
-    // 256 threads, one bin each: parallel exclusive scans of the slot counts
-    // and of the work units (no serial loop, no dependent global round trips).
-    __shared__ uint64_t wpos[4], witem[4];
-    __shared__ uint64_t s_start[kNB], s_count[kNB];
     BinTable* bt = so.bt;
     const int b = threadIdx.x, lane = b & 63, w = b >> 6;
-    uint64_t cnt = 0, kc = 0;
-    if (b < kNB) {
-        cnt = bt->hist[b];
-        const uint32_t ko = bt->kobs[b];
-        kc = b <= 32 ? uint64_t(b == 0 ? 1 : b) : (ko ? ko : bin_kmax(b));
-        bt->hist[b] = 0;   // ready for the next launch (stream-ordered)
-        bt->kobs[b] = 0;
-    }
-    const uint64_t oct = (cnt + kG - 1) / kG;
-    const uint64_t pos_c = oct * kG;
-    const uint64_t item_c = b >= 2 ? oct * (kc + kOctetCost) : 0;   // bins 0-1: tiny kernel
-    uint64_t ps = pos_c, is = item_c;
+    uint64_t cnt = 0, kc = 0, ps = 0, is = 0, pos_c = 0, item_c = 0;
+    if (b < 256) {
+        if (b < kNB) {
+            cnt = bt->hist[b];
+            const uint32_t ko = bt->kobs[b];
+            kc = b <= 32 ? uint64_t(b == 0 ? 1 : b) : (ko ? ko : bin_kmax(b));
+        }
+        const uint64_t oct = (cnt + kG - 1) / kG;
+        pos_c = oct * kG;
+        item_c = b >= 2 ? oct * (kc + kOctetCost) : 0;   // bins 0-1: the tiny phase
+        ps = pos_c;
+        is = item_c;
 #pragma unroll
-    for (int s = 1; s < 64; s <<= 1) {
-        const uint64_t a1 = __shfl_up(ps, s, kWaveSize);
-        const uint64_t a2 = __shfl_up(is, s, kWaveSize);
-        if (lane >= s) {
-            ps += a1;
-            is += a2;
+        for (int s = 1; s < 64; s <<= 1) {
+            const uint64_t a1 = __shfl_up(ps, s, kWaveSize);
+            const uint64_t a2 = __shfl_up(is, s, kWaveSize);
+            if (lane >= s) {
+                ps += a1;
+                is += a2;
+            }
+        }
+        if (lane == 63) {
+            sc.wpos[w] = ps;
+            sc.witem[w] = is;
         }
     }
-    if (lane == 63) {
-        wpos[w] = ps;
-        witem[w] = is;
-    }
     __syncthreads();
-    uint64_t pb = 0, ib = 0;
-    for (int j = 0; j < w; j++) {
-        pb += wpos[j];
-        ib += witem[j];
-    }
-    const uint64_t start = pb + ps - pos_c, items = ib + is - item_c;
     if (b < kNB) {
-        bt->start[b] = start;
-        bt->count[b] = cnt;
-        bt->cursor[b] = start;
-        bt->items[b] = items;
-        bt->kcost[b] = kc + kOctetCost;
-        s_start[b] = start;
-        s_count[b] = cnt;
+        uint64_t pb = 0, ib = 0;
+        for (int j = 0; j < w; j++) {
+            pb += sc.wpos[j];
+            ib += sc.witem[j];
+        }
+        const uint64_t start = pb + ps - pos_c, items = ib + is - item_c;
+        sc.start[b] = start;
+        sc.count[b] = cnt;
+        if (publish) {
+            bt->start[b] = start;
+            bt->count[b] = cnt;
+            bt->items[b] = items;
+            bt->kcost[b] = kc + kOctetCost;
+            if (b == kNB - 1)
+                bt->items[kNB] = items + item_c;
+        }
     }
-    if (b == kNB - 1)
-        bt->items[kNB] = items + item_c;
     __syncthreads();
-    // padding slots of each bin's last octet: empty
-    for (int t = threadIdx.x; t < kNB * kG; t += blockDim.x) {
-        const int bb = t / kG, j = t % kG;
-        const uint64_t c = s_count[bb];
-        const uint64_t slot = c + uint64_t(j);
-        if ((c % kG) && slot < (c + kG - 1) / kG * kG) {
-            so.desc[s_start[bb] + slot] = u32x4{0u, 0u, 0u, 0u};
-            so.idx[s_start[bb] + slot] = kNoIdx;
+    if (publish) {
+        for (int t = threadIdx.x; t < kNB * kG; t += blockDim.x) {
+            const int bb = t / kG, j = t % kG;
+            const uint64_t c = sc.count[bb];
+            const uint64_t slot = c + uint64_t(j);
+            if ((c % kG) && slot < (c + kG - 1) / kG * kG) {
+                so.desc[sc.start[bb] + slot] = u32x4{0u, 0u, 0u, 0u};
+                so.idx[sc.start[bb] + slot] = kNoIdx;
+            }
         }
     }
 }
@@ -934,9 +944,10 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter(BatchDesc d, Sorted so
 {
     __shared__ uint32_t cnt[kNB];
     __shared__ uint64_t base[kNB];
+    __shared__ BinScratch sc;
     for (int t = threadIdx.x; t < kNB; t += blockDim.x)
         cnt[t] = 0;
-    __syncthreads();
+    bin_layout(so, sc, blockIdx.x == 0);
     const uint64_t tile = uint64_t(blockDim.x) * kBinPer;
     const uint64_t n = entry_count<kMode>(d);
     for (uint64_t t0 = uint64_t(blockIdx.x) * tile; t0 < n; t0 += uint64_t(gridDim.x) * tile) {
@@ -963,7 +974,8 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter(BatchDesc d, Sorted so
         __syncthreads();
         for (int t = threadIdx.x; t < kNB; t += blockDim.x)
             if (cnt[t]) {
-                base[t] = atomicAdd(reinterpret_cast<unsigned long long*>(&so.bt->cursor[t]),
+                base[t] = sc.start[t] +
+                          atomicAdd(reinterpret_cast<unsigned long long*>(&so.bt->cursor[t]),
                                     (unsigned long long)cnt[t]);
                 cnt[t] = 0;
             }
@@ -1510,6 +1522,15 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
 __global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc d, Sorted so)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsEntries];
+    if (blockIdx.x == 0) {
+        // the histogram and cursors of this launch are consumed: zero them
+        // for the next one (stream-ordered; nothing here reads them)
+        for (int t = threadIdx.x; t < kNB; t += blockDim.x) {
+            so.bt->hist[t] = 0;
+            so.bt->kobs[t] = 0;
+            so.bt->cursor[t] = 0;
+        }
+    }
     tiny_run(d, so, lds);
     if (so.bt->items[2] == so.bt->items[kNB])
         return;   // every entry is tiny (or large on the batch path)
@@ -1805,8 +1826,6 @@ int launch_binned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_lar
     if (grid > uint64_t(c->ncu))
         grid = c->ncu;
     hipLaunchKernelGGL(k_bin_count<kMode>, dim3(grid), dim3(kThreads), 0, s, d, so, skip_large);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(256), 0, s, so);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_bin_scatter<kMode>, dim3(grid), dim3(kThreads), 0, s, d, so, skip_large);
     HIPCHK(hipGetLastError());
