@@ -70,8 +70,11 @@ VARIANTS = {
     "u4_c17": ["RAMCRC_UNROLL=4", "RAMCRC_CHUNK_SHIFT=17"],
     "u4_c20": ["RAMCRC_UNROLL=4", "RAMCRC_CHUNK_SHIFT=20"],
     # parallel-walk sync search (k_walk_sync)
-    "sh4": ["RAMCRC_SYNC_HOPS=4"],
+    "walkdbg": ["RAMCRC_WALK_DEBUG=1"],
     "sh5": ["RAMCRC_SYNC_HOPS=5"],
+    "sh7": ["RAMCRC_SYNC_HOPS=7"],
+    "sh8": ["RAMCRC_SYNC_HOPS=8"],
+    "sh10": ["RAMCRC_SYNC_HOPS=10"],
     "sp16": ["RAMCRC_SYNC_PER=16"],
     "sp4": ["RAMCRC_SYNC_PER=4"],
     "ss6": ["RAMCRC_SYNC_STAGE_KIB=6"],

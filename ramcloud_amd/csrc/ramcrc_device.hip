@@ -2171,6 +2171,8 @@ constexpr int kSyncPer = RAMCRC_SYNC_PER;           // candidates per lane per r
 constexpr uint32_t kSyncRound = kSyncPer * kWaveSize;   // 512 candidates
 static_assert(kSyncPer % 4 == 0 && kSyncPer <= 32, "candidates per lane: whole dwords");
 constexpr uint32_t kSyncSpan = 16384;               // candidate bytes searched per part
+constexpr uint32_t kMeetMax = 4;                    // B's fast path: meets within 4 records
+constexpr uint32_t kMeetHops = 3;                   // ... after at most 3 entries walked
 constexpr uint32_t kRewalkBudget = 1u << 15;        // hops B may re-walk before falling back
 constexpr uint32_t kNumTypes = 12;                  // TOTAL_LOG_ENTRY_TYPES, src/LogEntryTypes.h:68
 // part flags
@@ -2484,16 +2486,23 @@ __global__ __launch_bounds__(kSyncWaves * kWaveSize) void k_walk_sync(PWalk w)
 // one lane: fills the part result (count, metadata bytes and raw CRC, exit,
 // wrap / overrun flags) and hands every record to sink(index, offset,
 // length, header byte).
-template <class Sink>
-__device__ __forceinline__ void walk_lane(const PWalk& w, const uint32_t* tab, uint64_t seg,
-                                          uint64_t sb, uint32_t pos, uint32_t stop, PartRes& r,
-                                          Sink&& sink, uint32_t budget)
+// seg_peek on one segment.
+struct GlobalPeek {
+    uint64_t sb;
+    uint32_t capacity;
+    __device__ uint64_t operator()(uint32_t p) const { return seg_peek(sb, p, capacity); }
+};
+
+template <class Sink, class Peek>
+__device__ __forceinline__ void walk_lane(const PWalk& w, const uint32_t* tab, uint32_t pos,
+                                          uint32_t stop, PartRes& r, Sink&& sink, uint32_t budget,
+                                          Peek&& peek)
 {
     uint32_t count = 0, nmeta = 0, raw = 0, flags = kPartWalked, hops = 0;
     // The next header's load is issued before this entry's record store:
     // vmcnt counts stores too, so a wait for a load issued after a store
     // would also wait for the store to complete.
-    uint64_t q = pos < stop ? seg_peek(sb, pos, w.capacity) : 0ull;
+    uint64_t q = pos < stop ? peek(pos) : 0ull;
     while (pos < stop) {
         if (hops++ >= budget) {
             flags |= kPartWrap;   // out of budget: the serial walker takes the segment
@@ -2511,7 +2520,7 @@ __device__ __forceinline__ void walk_lane(const PWalk& w, const uint32_t* tab, u
             break;
         }
         const uint32_t next = uint32_t(h.next);
-        const uint64_t qn = next < stop ? seg_peek(sb, next, w.capacity) : 0ull;
+        const uint64_t qn = next < stop ? peek(next) : 0ull;
         sink(count, pos, h.len, uint32_t(q) & 0xFF);
         count++;
         pos = next;
@@ -2523,6 +2532,46 @@ __device__ __forceinline__ void walk_lane(const PWalk& w, const uint32_t* tab, u
     r.raw = raw;
     r.flags = flags;
 }
+
+template <class Sink>
+__device__ __forceinline__ void walk_lane(const PWalk& w, const uint32_t* tab, uint64_t seg,
+                                          uint64_t sb, uint32_t pos, uint32_t stop, PartRes& r,
+                                          Sink&& sink, uint32_t budget)
+{
+    walk_lane(w, tab, pos, stop, r, sink, budget, GlobalPeek{sb, w.capacity});
+}
+
+// B's re-walks are wave-uniform (every lane chases the same chain), so the
+// wave stages the segment bytes around the chain in LDS, kFixWin at a time,
+// and each hop reads LDS instead of waiting a memory round trip.
+constexpr uint32_t kFixWin = 16384;
+struct WinPeek {
+    uint8_t* lds;
+    uint64_t sb;
+    uint32_t capacity;
+    uint32_t wb;   // staged [wb, wb + kFixWin); kNoStart: nothing staged
+    __device__ uint64_t operator()(uint32_t p)
+    {
+        if (wb == kNoStart || p < wb || ((p - wb) & ~3u) + 8 > kFixWin) {
+            const uint32_t b = p & ~15u;
+            const uint32_t l16 = (threadIdx.x & (kWaveSize - 1)) * 16;
+            u32x4 v[kFixWin / 1024];
+#pragma unroll
+            for (uint32_t u = 0; u < kFixWin / 1024; u++) {
+                const uint64_t a = uint64_t(b) + u * 1024 + l16;
+                v[u] = a + 16 <= capacity ? load16(sb + a) : u32x4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kFixWin / 1024; u++)
+                *reinterpret_cast<u32x4*>(lds + u * 1024 + l16) = v[u];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            wb = b;
+        }
+        const uint32_t o = p - wb;
+        const uint32_t* w32 = reinterpret_cast<const uint32_t*>(lds + (o & ~3u));
+        return ((uint64_t(w32[1]) << 32) | w32[0]) >> (8 * (o & 3));
+    }
+};
 
 struct NoSink {
     __device__ void operator()(uint32_t, uint32_t, uint32_t, uint32_t) const {}
@@ -2606,21 +2655,31 @@ __global__ __launch_bounds__(256) void k_walk_parts(PWalk w)
     }
 }
 
+#ifdef RAMCRC_WALK_DEBUG
+__device__ unsigned long long g_fixdbg[8];
+#endif
+
 // B: one wave per segment.
 __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
 {
     __shared__ uint32_t tab[4 * 256];
+    __shared__ __attribute__((aligned(16))) uint8_t win[kFixWin];
     walk_tab_fill(tab);
     const int lane = threadIdx.x;
     for (uint64_t seg = blockIdx.x; seg < w.nseg; seg += gridDim.x) {
         const uint32_t limit = walk_limit(w, seg);
         const ramcrc_seg_cert cert = w.certs[seg];
         const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
+        WinPeek wpeek{win, sb, w.capacity, kNoStart};
         PartRes* parts = w.parts + seg * w.nparts;
         // The true chain (wave-uniform): pos, the metadata CRC so far (raw
         // state from 0xFFFFFFFF), the records before the current part.
         uint32_t pos = 0, crc = 0xFFFFFFFFu, count = 0, rewalk = 0;
         bool overrun = false, fallback = false;
+#ifdef RAMCRC_WALK_DEBUG
+        uint32_t dbg_meet = 0, dbg_meet_hops = 0, dbg_chase = 0, dbg_miss = 0;
+        const uint64_t dbg_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
         // Fold the accepted parts of a chunk (one per lane) into crc in one
         // step: crc <- X^n(crc) ^ sum_j X^(suffix_j)(raw_j), suffix_j = the
         // metadata bytes of the accepted parts after j, n = all of them.
@@ -2641,28 +2700,64 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
             crc = mulmod_horner(crc, xpow8_dev(n_all)) ^ c;
         };
         // Fast path -- every well-formed segment: part 0 starts at 0, every
-        // part below the limit was walked from exactly where the part before
-        // it stopped (inside itself), none wrapped and only the last may have
-        // overrun.  Checked for all parts at once, then accepted as walked.
+        // part below the limit was walked from where the part before it
+        // stopped (inside itself) or met that offset within its first
+        // kMeetMax recorded entries (a junk guess whose length lands on the
+        // true chain: the common misguess), none wrapped and only the last
+        // may have overrun.  Checked for all parts at once, then accepted.
         const uint32_t nlive =
             limit == 0 ? 0u : uint32_t((uint64_t(limit) + kPartBytes - 1) >> kPartShift);
+        // Where the chain arriving at pe meets part k's guessed chain: after
+        // `hops` (<= kMeetHops) entries walked from pe, at the guess's record
+        // `cut` (0: the guess itself, up to kMeetMax); -1 when it does not.
+        // The walked entries' header + length bytes: raw CRC wr over wn bytes.
+        auto meet_at = [&](uint32_t k, uint32_t st, uint32_t fl, uint32_t gc, uint32_t pe,
+                           uint32_t& wr, uint32_t& wn) -> int {
+            wr = wn = 0;
+            if (!(fl & kPartWalked))
+                return -1;
+            // a spilled part's records are not in the scratch: met at its start only
+            const uint32_t gn = (fl & kPartSpill) ? 0u : (gc < kPartRec ? gc : kPartRec);
+            const uint64_t base = (uint64_t(seg) * w.nparts + k) * kPartRec;
+            const uint64_t Ek = (uint64_t(k) << kPartShift) + kPartBytes;
+            uint32_t p = pe;
+            for (uint32_t hh = 0;; hh++) {
+                if (p == st)
+                    return int(hh << 8);
+                for (uint32_t c = 1; c <= kMeetMax && c < gn; c++)
+                    if (w.recs[base + c].x == p)
+                        return int((hh << 8) | c);
+                if (hh == kMeetHops || p >= limit || uint64_t(p) >= Ek)
+                    return -1;
+                const uint64_t q = seg_peek(sb, p, w.capacity);
+                const Hop h = hop_of(q, p);
+                if (h.next > w.capacity)
+                    return -1;
+                wr = meta_update(tab, wr, q, h.mbytes);
+                wn += h.mbytes;
+                p = uint32_t(h.next);
+            }
+        };
         bool fast = true;
         {
             uint32_t prev = 0;   // exit of the part before the chunk
             for (uint32_t k0 = 0; k0 < nlive && fast; k0 += kWaveSize) {
                 const uint32_t k = k0 + uint32_t(lane);
                 const bool in = k < nlive;
-                uint32_t st = 0, ex = 0, fl = 0;
+                uint32_t st = 0, ex = 0, fl = 0, gc = 0;
                 if (in) {
                     st = parts[k].start;
                     ex = parts[k].exit;
                     fl = parts[k].flags;
+                    gc = parts[k].count;
                 }
                 uint32_t pe = __shfl_up(ex, 1, kWaveSize);
                 pe = lane == 0 ? prev : pe;
                 const uint64_t Ek = (uint64_t(k) << kPartShift) + kPartBytes;
-                const bool ok = !in || ((fl & kPartWalked) && !(fl & kPartWrap) && st == pe &&
-                                        uint64_t(pe) < Ek && (k + 1 == nlive || !(fl & kPartOverrun)));
+                uint32_t wr, wn;
+                const bool ok = !in || ((fl & kPartWalked) && !(fl & kPartWrap) && uint64_t(pe) < Ek &&
+                                        (k + 1 == nlive || !(fl & kPartOverrun)) &&
+                                        meet_at(k, st, fl, gc, pe, wr, wn) >= 0);
                 fast = __ballot(!ok) == 0;
                 const uint32_t last = nlive - 1 - k0 < uint32_t(kWaveSize - 1) ? nlive - 1 - k0
                                                                                 : uint32_t(kWaveSize - 1);
@@ -2670,12 +2765,39 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
             }
         }
         if (fast) {
+            uint32_t prev = 0;
             for (uint32_t k0 = 0; k0 < nlive; k0 += kWaveSize) {
                 const uint32_t k = k0 + uint32_t(lane);
                 const bool in = k < nlive;
                 PartRes r{};
                 if (in)
                     r = parts[k];
+                uint32_t pe = __shfl_up(r.exit, 1, kWaveSize);
+                pe = lane == 0 ? prev : pe;
+                uint32_t wr = 0, wn = 0;
+                const int mt = in ? meet_at(k, r.start, r.flags, r.count, pe, wr, wn) : 0;
+                const uint32_t hops = uint32_t(mt) >> 8, cut = uint32_t(mt) & 0xFF;
+                if (mt > 0) {
+                    // drop the guess's first `cut` entries (junk), whose header +
+                    // length bytes are rebuilt from the records, and put the
+                    // `hops` entries walked from pe in front:
+                    // raw(0, A||B) = X^|B|(raw(0, A)) ^ raw(0, B)
+                    const uint64_t base = (uint64_t(seg) * w.nparts + k) * kPartRec;
+                    uint32_t jr = 0, jn = 0;
+                    for (uint32_t e = 0; e < cut; e++) {
+                        const uint2 g = w.recs[base + e];
+                        const uint32_t mb = ((g.y >> 6) & 3) + 2;
+                        const uint64_t qe = uint64_t(g.y & 0xFF) | (uint64_t(g.y >> 8) << 8);
+                        jr = meta_update(tab, jr, qe, mb);
+                        jn += mb;
+                    }
+                    const uint32_t tn = r.nmeta - jn;
+                    const uint32_t tr = r.raw ^ mulmod_horner(jr, xpow8_dev(tn));
+                    r.raw = mulmod_horner(wr, xpow8_dev(tn)) ^ tr;
+                    r.nmeta = wn + tn;
+                    r.count = hops + r.count - cut;
+                    r.start = pe;
+                }
                 const uint32_t c = in ? r.count : 0u;
                 uint32_t incl = c;   // inclusive prefix of the record counts
 #pragma unroll
@@ -2690,11 +2812,13 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
                 if (in) {
                     r.rec = count + incl - c;
                     r.flags |= kPartEmit;
-                    r.pre = r.cut = 0;
+                    r.pre = hops;   // walked again (and emitted) by C
+                    r.cut = cut;
                     parts[k] = r;
                 }
                 count += __shfl(incl, int(last), kWaveSize);
                 pos = __shfl(r.exit, int(last), kWaveSize);
+                prev = pos;
                 overrun = (__shfl(r.flags, int(last), kWaveSize) & kPartOverrun) != 0;
             }
         }
@@ -2731,7 +2855,9 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
                         // its entries from there on are the true chain's.  Without
                         // a meeting the walk covers the part (a full re-walk).
                         const uint32_t gc = __builtin_amdgcn_readlane(r.count, j);
-                        const uint32_t gn = gc < kPartRec ? gc : kPartRec;
+                        // a spilled part's records are not in the scratch: it
+                        // can only be met at its start
+                        const uint32_t gn = (fl & kPartSpill) ? 0u : (gc < kPartRec ? gc : kPartRec);
                         const uint64_t pidx = uint64_t(seg) * w.nparts + k0 + j;
                         uint2 g = make_uint2(0xFFFFFFFFu, 0u);
                         if (uint32_t(lane) < gn)
@@ -2752,7 +2878,7 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
                                 wflags |= kPartWrap;   // out of budget: the serial walker
                                 break;
                             }
-                            const uint64_t q = seg_peek(sb, p, w.capacity);
+                            const uint64_t q = wpeek(p);
                             const Hop h = hop_of(q, p);
                             wr = meta_update(tab, wr, q, h.mbytes);
                             wn += h.mbytes;
@@ -2768,6 +2894,14 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
                             p = uint32_t(h.next);
                         }
                         rewalk += wc + 1;
+#ifdef RAMCRC_WALK_DEBUG
+                        if (cut >= 0) {
+                            dbg_meet++;
+                            dbg_meet_hops += wc;
+                        } else {
+                            dbg_chase++;
+                        }
+#endif
                         if (cut >= 0) {
                             // the guess's totals minus its first `cut` entries, whose
                             // header + length bytes are folded from the records:
@@ -2826,9 +2960,12 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
                     // misguessed: walk this part again from the true offset
                     const uint32_t stop = Ej < limit ? Ej : limit;
                     PartRes x;
-                    walk_lane(w, tab, seg, sb, pos, stop, x, NoSink{},
-                              rewalk < kRewalkBudget ? kRewalkBudget - rewalk : 0u);
+                    walk_lane(w, tab, pos, stop, x, NoSink{},
+                              rewalk < kRewalkBudget ? kRewalkBudget - rewalk : 0u, wpeek);
                     rewalk += x.count + 1;
+#ifdef RAMCRC_WALK_DEBUG
+                    dbg_miss++;
+#endif
                     xexit = x.exit;
                     xcount = x.count;
                     xflags = x.flags;
@@ -2862,6 +2999,26 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
             if (k < w.nparts)
                 parts[k] = r;
         }
+#ifdef RAMCRC_WALK_DEBUG
+        const uint64_t dbg_t1 = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+            const unsigned long long dt = dbg_t1 - dbg_t0;
+            atomicMax(&g_fixdbg[fast ? 0 : 1], dt);
+            atomicAdd(&g_fixdbg[fast ? 2 : 3], 1ull);
+            atomicAdd(&g_fixdbg[fast ? 4 : 5], dt);
+            if (!fast)
+                printf("fixdbg seg=%u meet=%u meet_hops=%u chase=%u miss=%u rewalk=%u us=%.1f\n",
+                       uint32_t(seg), dbg_meet, dbg_meet_hops, dbg_chase, dbg_miss, rewalk,
+                       double(dt) / 100.0);
+            if (atomicAdd(&g_fixdbg[7], 1ull) == w.nseg - 1) {
+                printf("fixsum fast n=%llu max=%.1fus avg=%.1fus slow n=%llu max=%.1fus avg=%.1fus\n",
+                       g_fixdbg[2], g_fixdbg[0] / 100.0, g_fixdbg[4] / 100.0 / (g_fixdbg[2] + 1e-9),
+                       g_fixdbg[3], g_fixdbg[1] / 100.0, g_fixdbg[5] / 100.0 / (g_fixdbg[3] + 1e-9));
+                for (int t = 0; t < 8; t++)
+                    g_fixdbg[t] = 0;
+            }
+        }
+#endif
         if (fallback) {
             if (lane == 0)
                 w.fallback[seg] = 1;
