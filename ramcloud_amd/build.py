@@ -71,6 +71,8 @@ VARIANTS = {
     "u4_c20": ["RAMCRC_UNROLL=4", "RAMCRC_CHUNK_SHIFT=20"],
     # parallel-walk sync search (k_walk_sync)
     "walkdbg": ["RAMCRC_WALK_DEBUG=1"],
+    "fw32": ["RAMCRC_FIX_WIN_KIB=32"],
+    "fw8": ["RAMCRC_FIX_WIN_KIB=8"],
     "sh5": ["RAMCRC_SYNC_HOPS=5"],
     "sh7": ["RAMCRC_SYNC_HOPS=7"],
     "sh8": ["RAMCRC_SYNC_HOPS=8"],

@@ -2544,7 +2544,10 @@ __device__ __forceinline__ void walk_lane(const PWalk& w, const uint32_t* tab, u
 // B's re-walks are wave-uniform (every lane chases the same chain), so the
 // wave stages the segment bytes around the chain in LDS, kFixWin at a time,
 // and each hop reads LDS instead of waiting a memory round trip.
-constexpr uint32_t kFixWin = 16384;
+#ifndef RAMCRC_FIX_WIN_KIB
+#define RAMCRC_FIX_WIN_KIB 16
+#endif
+constexpr uint32_t kFixWin = RAMCRC_FIX_WIN_KIB * 1024;
 struct WinPeek {
     uint8_t* lds;
     uint64_t sb;
@@ -2659,7 +2662,18 @@ __global__ __launch_bounds__(256) void k_walk_parts(PWalk w)
 __device__ unsigned long long g_fixdbg[8];
 #endif
 
-// B: one wave per segment.
+// B: one wave per segment, lane k deciding part k of a chunk of 64.  A part
+// is accepted as A walked it when the true chain arrives at its guess, or
+// meets the guessed chain within kMeetHops entries at one of its first
+// kMeetMax records (a junk guess whose length lands on the true chain: the
+// common misguess); the true arrival offset of part k is the exit of part
+// k-1 as A walked it, so every part is checked at once.  The parts that
+// fail -- a guess that never meets, a part the chain jumps over, a part left
+// unwalked -- are resolved in order by the whole wave (re-walked from the
+// true offset through an LDS window), each resolution re-checking the part
+// after it.  The accepted parts' metadata CRCs fold into the segment's with
+// one GF(2) multiply per part, then the status is written and the records
+// are allocated (one atomic per segment).
 __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
 {
     __shared__ uint32_t tab[4 * 256];
@@ -2673,11 +2687,12 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
         WinPeek wpeek{win, sb, w.capacity, kNoStart};
         PartRes* parts = w.parts + seg * w.nparts;
         // The true chain (wave-uniform): pos, the metadata CRC so far (raw
-        // state from 0xFFFFFFFF), the records before the current part.
+        // state from 0xFFFFFFFF), the records before the current chunk.
         uint32_t pos = 0, crc = 0xFFFFFFFFu, count = 0, rewalk = 0;
         bool overrun = false, fallback = false;
 #ifdef RAMCRC_WALK_DEBUG
         uint32_t dbg_meet = 0, dbg_meet_hops = 0, dbg_chase = 0, dbg_miss = 0;
+        bool fast = true;
         const uint64_t dbg_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
         // Fold the accepted parts of a chunk (one per lane) into crc in one
@@ -2699,14 +2714,6 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
                 c ^= __shfl_xor(c, s, kWaveSize);
             crc = mulmod_horner(crc, xpow8_dev(n_all)) ^ c;
         };
-        // Fast path -- every well-formed segment: part 0 starts at 0, every
-        // part below the limit was walked from where the part before it
-        // stopped (inside itself) or met that offset within its first
-        // kMeetMax recorded entries (a junk guess whose length lands on the
-        // true chain: the common misguess), none wrapped and only the last
-        // may have overrun.  Checked for all parts at once, then accepted.
-        const uint32_t nlive =
-            limit == 0 ? 0u : uint32_t((uint64_t(limit) + kPartBytes - 1) >> kPartShift);
         // Where the chain arriving at pe meets part k's guessed chain: after
         // `hops` (<= kMeetHops) entries walked from pe, at the guess's record
         // `cut` (0: the guess itself, up to kMeetMax); -1 when it does not.
@@ -2714,12 +2721,12 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
         auto meet_at = [&](uint32_t k, uint32_t st, uint32_t fl, uint32_t gc, uint32_t pe,
                            uint32_t& wr, uint32_t& wn) -> int {
             wr = wn = 0;
-            if (!(fl & kPartWalked))
+            const uint64_t Ek = (uint64_t(k) << kPartShift) + kPartBytes;
+            if (!(fl & kPartWalked) || (fl & kPartWrap) || uint64_t(pe) >= Ek)
                 return -1;
             // a spilled part's records are not in the scratch: met at its start only
             const uint32_t gn = (fl & kPartSpill) ? 0u : (gc < kPartRec ? gc : kPartRec);
             const uint64_t base = (uint64_t(seg) * w.nparts + k) * kPartRec;
-            const uint64_t Ek = (uint64_t(k) << kPartShift) + kPartBytes;
             uint32_t p = pe;
             for (uint32_t hh = 0;; hh++) {
                 if (p == st)
@@ -2738,266 +2745,273 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
                 p = uint32_t(h.next);
             }
         };
-        bool fast = true;
-        {
-            uint32_t prev = 0;   // exit of the part before the chunk
-            for (uint32_t k0 = 0; k0 < nlive && fast; k0 += kWaveSize) {
-                const uint32_t k = k0 + uint32_t(lane);
-                const bool in = k < nlive;
-                uint32_t st = 0, ex = 0, fl = 0, gc = 0;
-                if (in) {
-                    st = parts[k].start;
-                    ex = parts[k].exit;
-                    fl = parts[k].flags;
-                    gc = parts[k].count;
-                }
-                uint32_t pe = __shfl_up(ex, 1, kWaveSize);
-                pe = lane == 0 ? prev : pe;
-                const uint64_t Ek = (uint64_t(k) << kPartShift) + kPartBytes;
-                uint32_t wr, wn;
-                const bool ok = !in || ((fl & kPartWalked) && !(fl & kPartWrap) && uint64_t(pe) < Ek &&
-                                        (k + 1 == nlive || !(fl & kPartOverrun)) &&
-                                        meet_at(k, st, fl, gc, pe, wr, wn) >= 0);
-                fast = __ballot(!ok) == 0;
-                const uint32_t last = nlive - 1 - k0 < uint32_t(kWaveSize - 1) ? nlive - 1 - k0
-                                                                                : uint32_t(kWaveSize - 1);
-                prev = __shfl(ex, int(last), kWaveSize);
-            }
-        }
-        if (fast) {
-            uint32_t prev = 0;
-            for (uint32_t k0 = 0; k0 < nlive; k0 += kWaveSize) {
-                const uint32_t k = k0 + uint32_t(lane);
-                const bool in = k < nlive;
-                PartRes r{};
-                if (in)
-                    r = parts[k];
-                uint32_t pe = __shfl_up(r.exit, 1, kWaveSize);
-                pe = lane == 0 ? prev : pe;
-                uint32_t wr = 0, wn = 0;
-                const int mt = in ? meet_at(k, r.start, r.flags, r.count, pe, wr, wn) : 0;
-                const uint32_t hops = uint32_t(mt) >> 8, cut = uint32_t(mt) & 0xFF;
-                if (mt > 0) {
-                    // drop the guess's first `cut` entries (junk), whose header +
-                    // length bytes are rebuilt from the records, and put the
-                    // `hops` entries walked from pe in front:
-                    // raw(0, A||B) = X^|B|(raw(0, A)) ^ raw(0, B)
-                    const uint64_t base = (uint64_t(seg) * w.nparts + k) * kPartRec;
-                    uint32_t jr = 0, jn = 0;
-                    for (uint32_t e = 0; e < cut; e++) {
-                        const uint2 g = w.recs[base + e];
-                        const uint32_t mb = ((g.y >> 6) & 3) + 2;
-                        const uint64_t qe = uint64_t(g.y & 0xFF) | (uint64_t(g.y >> 8) << 8);
-                        jr = meta_update(tab, jr, qe, mb);
-                        jn += mb;
-                    }
-                    const uint32_t tn = r.nmeta - jn;
-                    const uint32_t tr = r.raw ^ mulmod_horner(jr, xpow8_dev(tn));
-                    r.raw = mulmod_horner(wr, xpow8_dev(tn)) ^ tr;
-                    r.nmeta = wn + tn;
-                    r.count = hops + r.count - cut;
-                    r.start = pe;
-                }
-                const uint32_t c = in ? r.count : 0u;
-                uint32_t incl = c;   // inclusive prefix of the record counts
-#pragma unroll
-                for (int s = 1; s < kWaveSize; s <<= 1) {
-                    const uint32_t y = __shfl_up(incl, s, kWaveSize);
-                    if (lane >= s)
-                        incl += y;
-                }
-                fold(in, r.nmeta, r.raw);
-                const uint32_t last = nlive - 1 - k0 < uint32_t(kWaveSize - 1) ? nlive - 1 - k0
-                                                                                : uint32_t(kWaveSize - 1);
-                if (in) {
-                    r.rec = count + incl - c;
-                    r.flags |= kPartEmit;
-                    r.pre = hops;   // walked again (and emitted) by C
-                    r.cut = cut;
-                    parts[k] = r;
-                }
-                count += __shfl(incl, int(last), kWaveSize);
-                pos = __shfl(r.exit, int(last), kWaveSize);
-                prev = pos;
-                overrun = (__shfl(r.flags, int(last), kWaveSize) & kPartOverrun) != 0;
-            }
-        }
-        for (uint32_t k0 = 0; !fast && k0 < w.nparts && pos < limit && !overrun && !fallback;
-             k0 += kWaveSize) {
+        const uint32_t nlive =
+            limit == 0 ? 0u : uint32_t((uint64_t(limit) + kPartBytes - 1) >> kPartShift);
+        for (uint32_t k0 = 0; k0 < nlive && !overrun && !fallback; k0 += kWaveSize) {
             const uint32_t k = k0 + uint32_t(lane);
+            const bool in = k < nlive;
             PartRes r{};
-            if (k < w.nparts)
+            if (in)
                 r = parts[k];
-            // Decide part by part; a part walked again is walked by every
-            // lane on the same addresses and kept by the part's lane.
-            const uint32_t jn = w.nparts - k0 < uint32_t(kWaveSize) ? w.nparts - k0 : kWaveSize;
-            for (uint32_t j = 0; j < jn; j++) {
-                if (pos >= limit || overrun || fallback)
+            const uint32_t gst = r.start;   // A's guess
+            // per lane: ok (decided), emit (accepted: walked or met), the
+            // meet to apply (mt >= 0; kResolved: totals already final), and
+            // the exit handed to the next part
+            constexpr int kResolved = -2;
+            uint32_t ex = r.exit, wr = 0, wn = 0;
+            int mt = -1;
+            {
+                uint32_t pe = __shfl_up(ex, 1, kWaveSize);
+                pe = lane == 0 ? pos : pe;
+                if (in)
+                    mt = meet_at(k, gst, r.flags, r.count, pe, wr, wn);
+                if (mt > 0)
+                    r.start = pe;
+            }
+            bool ok = !in || mt >= 0, emit = in && mt >= 0;
+            while (true) {
+                // the first undecided part; every part before it is decided
+                const uint64_t bad = __ballot(!ok);
+                if (!bad)
                     break;
-                const uint64_t Ej64 = (uint64_t(k0 + j) << kPartShift) + kPartBytes;
-                if (pos >= Ej64)
-                    continue;   // the chain jumps over this part
-                const uint32_t Ej = uint32_t(Ej64 < w.capacity ? Ej64 : w.capacity);
-                const uint32_t st = __builtin_amdgcn_readlane(r.start, j);
-                const uint32_t fl = __builtin_amdgcn_readlane(r.flags, j);
-                uint32_t xexit = 0, xcount = 0, xflags = 0;
-                bool have = false;
-                if (fl & kPartWalked) {
-                    if (st == pos) {
-                        xexit = __builtin_amdgcn_readlane(r.exit, j);
-                        xcount = __builtin_amdgcn_readlane(r.count, j);
-                        xflags = fl;
-                        have = true;
-                    } else {
-                        // Walk from pos (wave-uniform) until the chain meets the
-                        // guessed one: at one of the offsets A recorded for it
-                        // (lane e holds its e-th entry; the first is the guess);
-                        // its entries from there on are the true chain's.  Without
-                        // a meeting the walk covers the part (a full re-walk).
-                        const uint32_t gc = __builtin_amdgcn_readlane(r.count, j);
-                        // a spilled part's records are not in the scratch: it
-                        // can only be met at its start
-                        const uint32_t gn = (fl & kPartSpill) ? 0u : (gc < kPartRec ? gc : kPartRec);
-                        const uint64_t pidx = uint64_t(seg) * w.nparts + k0 + j;
-                        uint2 g = make_uint2(0xFFFFFFFFu, 0u);
-                        if (uint32_t(lane) < gn)
-                            g = w.recs[pidx * kPartRec + uint32_t(lane)];
-                        const uint32_t stop = Ej < limit ? Ej : limit;
-                        const uint32_t budget = rewalk < kRewalkBudget ? kRewalkBudget - rewalk : 0u;
-                        uint32_t p = pos, wc = 0, wn = 0, wr = 0, wflags = kPartWalked;
-                        int cut = -1;
-                        while (true) {
-                            const uint64_t hit = __ballot(uint32_t(lane) < gn && g.x == p);
-                            if (hit || (gn == 0 && p == st)) {
-                                cut = hit ? int(__builtin_ctzll(hit)) : 0;
-                                break;
-                            }
-                            if (p >= stop)
-                                break;
-                            if (wc >= budget) {
-                                wflags |= kPartWrap;   // out of budget: the serial walker
-                                break;
-                            }
-                            const uint64_t q = wpeek(p);
-                            const Hop h = hop_of(q, p);
-                            wr = meta_update(tab, wr, q, h.mbytes);
-                            wn += h.mbytes;
-                            if (h.next > 0xFFFFFFFFull) {
-                                wflags |= kPartWrap;
-                                break;
-                            }
-                            if (h.next > w.capacity) {
-                                wflags |= kPartOverrun;
-                                break;
-                            }
-                            wc++;
-                            p = uint32_t(h.next);
-                        }
-                        rewalk += wc + 1;
+                const int j = int(__builtin_ctzll(bad));
+                // an accepted part below it that overran ends the chain
+                const uint64_t ovr = __ballot(emit && (r.flags & kPartOverrun));
+                if (ovr && int(__builtin_ctzll(ovr)) < j)
+                    break;
 #ifdef RAMCRC_WALK_DEBUG
-                        if (cut >= 0) {
-                            dbg_meet++;
-                            dbg_meet_hops += wc;
-                        } else {
-                            dbg_chase++;
-                        }
+                fast = false;
 #endif
-                        if (cut >= 0) {
-                            // the guess's totals minus its first `cut` entries, whose
-                            // header + length bytes are folded from the records:
-                            // raw(0, A||S) = X^|S|(raw(0, A)) ^ raw(0, S)
-                            const bool in = lane < cut;
-                            const uint32_t mb = in ? ((g.y >> 6) & 3) + 2 : 0u;
-                            const uint64_t qe = uint64_t(g.y & 0xFF) | (uint64_t(g.y >> 8) << 8);
-                            const uint32_t re = in ? meta_update(tab, 0u, qe, mb) : 0u;
-                            uint32_t incl = mb;   // suffix sums of the prefix's bytes
-#pragma unroll
-                            for (int s = 1; s < kWaveSize; s <<= 1) {
-                                const uint32_t y = __shfl_down(incl, s, kWaveSize);
-                                if (lane + s < kWaveSize)
-                                    incl += y;
-                            }
-                            const uint32_t pn = __shfl(incl, 0, kWaveSize);
-                            uint32_t pr = in ? mulmod_horner(re, xpow8_dev(incl - mb)) : 0u;
-#pragma unroll
-                            for (int s = 1; s < kWaveSize; s <<= 1)
-                                pr ^= __shfl_xor(pr, s, kWaveSize);
-                            const uint32_t tn = __builtin_amdgcn_readlane(r.nmeta, j);
-                            const uint32_t tr = __builtin_amdgcn_readlane(r.raw, j);
-                            const uint32_t sn = tn - pn;   // suffix metadata bytes
-                            const uint32_t sr = tr ^ mulmod_horner(pr, xpow8_dev(sn));
-                            xexit = __builtin_amdgcn_readlane(r.exit, j);
-                            xcount = wc + gc - uint32_t(cut);
-                            xflags = fl;
-                            const uint32_t nn = wn + sn;
-                            const uint32_t rr = mulmod_horner(wr, xpow8_dev(sn)) ^ sr;
-                            if (lane == int(j)) {
-                                r.start = pos;
-                                r.count = xcount;
-                                r.nmeta = nn;
-                                r.raw = rr;
-                                r.pre = wc;
-                                r.cut = uint32_t(cut);
-                            }
-                        } else {
-                            // walked the whole part: C walks it once more
-                            xexit = p;
-                            xcount = wc;
-                            xflags = wflags;
-                            if (lane == int(j)) {
-                                r.start = pos;
-                                r.exit = p;
-                                r.count = wc;
-                                r.nmeta = wn;
-                                r.raw = wr;
-                                r.flags = wflags | kPartChase;
-                            }
+                const uint32_t kj = k0 + uint32_t(j);
+                const uint32_t pe = j == 0 ? pos : uint32_t(__builtin_amdgcn_readlane(int(ex), j - 1));
+                const uint32_t st = uint32_t(__builtin_amdgcn_readlane(int(gst), j));
+                const uint32_t fl = uint32_t(__builtin_amdgcn_readlane(int(r.flags), j));
+                const uint64_t Ej64 = (uint64_t(kj) << kPartShift) + kPartBytes;
+                const uint32_t Ej = uint32_t(Ej64 < w.capacity ? Ej64 : w.capacity);
+                const uint32_t stop = Ej < limit ? Ej : limit;
+                const uint32_t budget = rewalk < kRewalkBudget ? kRewalkBudget - rewalk : 0u;
+                bool jemit = true;
+                uint32_t jex = pe;
+                if (uint64_t(pe) >= Ej64) {
+                    jemit = false;   // the chain jumps over this part
+                } else if (fl & kPartWalked) {
+                    // Walk from pe until the chain meets the guessed one at any
+                    // of the offsets A recorded for it (lane e holds its e-th
+                    // entry; the first is the guess); its entries from there on
+                    // are the true chain's.  Without a meeting the walk covers
+                    // the part (a full re-walk).
+                    const uint32_t gc = uint32_t(__builtin_amdgcn_readlane(int(r.count), j));
+                    const uint32_t gn = (fl & kPartSpill) ? 0u : (gc < kPartRec ? gc : kPartRec);
+                    const uint64_t pidx = uint64_t(seg) * w.nparts + kj;
+                    uint2 g = make_uint2(0xFFFFFFFFu, 0u);
+                    if (uint32_t(lane) < gn)
+                        g = w.recs[pidx * kPartRec + uint32_t(lane)];
+                    uint32_t p = pe, wc = 0, wnn = 0, wrr = 0, wflags = kPartWalked;
+                    int cut = -1;
+                    uint2 mine = make_uint2(0u, 0u);   // record wc of the walk, in lane wc
+                    bool huge = false;
+                    while (true) {
+                        const uint64_t hit = __ballot(uint32_t(lane) < gn && g.x == p);
+                        if (hit || (!(fl & kPartWrap) && p == st)) {
+                            cut = hit ? int(__builtin_ctzll(hit)) : 0;
+                            break;
                         }
-                        have = true;
+                        if (p >= stop)
+                            break;
+                        if (wc >= budget) {
+                            wflags |= kPartWrap;   // out of budget: the serial walker
+                            break;
+                        }
+                        const uint64_t q = wpeek(p);
+                        const Hop h = hop_of(q, p);
+                        wrr = meta_update(tab, wrr, q, h.mbytes);
+                        wnn += h.mbytes;
+                        if (h.next > 0xFFFFFFFFull) {
+                            wflags |= kPartWrap;
+                            break;
+                        }
+                        if (h.next > w.capacity) {
+                            wflags |= kPartOverrun;
+                            break;
+                        }
+                        if (uint32_t(lane) == wc)
+                            mine = make_uint2(p, (h.len << 8) | (uint32_t(q) & 0xFF));
+                        huge = huge || h.len >= (1u << 24);
+                        wc++;
+                        p = uint32_t(h.next);
                     }
-                }
-                if (!have) {
-                    // misguessed: walk this part again from the true offset
-                    const uint32_t stop = Ej < limit ? Ej : limit;
-                    PartRes x;
-                    walk_lane(w, tab, pos, stop, x, NoSink{},
-                              rewalk < kRewalkBudget ? kRewalkBudget - rewalk : 0u, wpeek);
-                    rewalk += x.count + 1;
+                    rewalk += wc + 1;
+                    if (cut >= 0 && (fl & kPartWrap)) {
+                        wflags |= kPartWrap;   // met a chain that wraps: the serial walker
+                    } else if (cut >= 0) {
+#ifdef RAMCRC_WALK_DEBUG
+                        dbg_meet++;
+                        dbg_meet_hops += wc;
+#endif
+                        // the guess's totals minus its first `cut` entries, whose
+                        // header + length bytes are folded from the records:
+                        // raw(0, A||S) = X^|S|(raw(0, A)) ^ raw(0, S)
+                        const bool inp = lane < cut;
+                        const uint32_t mb = inp ? ((g.y >> 6) & 3) + 2 : 0u;
+                        const uint64_t qe = uint64_t(g.y & 0xFF) | (uint64_t(g.y >> 8) << 8);
+                        const uint32_t re = inp ? meta_update(tab, 0u, qe, mb) : 0u;
+                        uint32_t incl = mb;   // suffix sums of the prefix's bytes
+#pragma unroll
+                        for (int s = 1; s < kWaveSize; s <<= 1) {
+                            const uint32_t y = __shfl_down(incl, s, kWaveSize);
+                            if (lane + s < kWaveSize)
+                                incl += y;
+                        }
+                        const uint32_t pn = __shfl(incl, 0, kWaveSize);
+                        uint32_t pr = inp ? mulmod_horner(re, xpow8_dev(incl - mb)) : 0u;
+#pragma unroll
+                        for (int s = 1; s < kWaveSize; s <<= 1)
+                            pr ^= __shfl_xor(pr, s, kWaveSize);
+                        const uint32_t tn = uint32_t(__builtin_amdgcn_readlane(int(r.nmeta), j));
+                        const uint32_t tr = uint32_t(__builtin_amdgcn_readlane(int(r.raw), j));
+                        const uint32_t sn = tn - pn;   // suffix metadata bytes
+                        const uint32_t sr = tr ^ mulmod_horner(pr, xpow8_dev(sn));
+                        jex = uint32_t(__builtin_amdgcn_readlane(int(r.exit), j));
+                        const uint32_t nn = wnn + sn;
+                        const uint32_t rr = mulmod_horner(wrr, xpow8_dev(sn)) ^ sr;
+                        if (lane == j) {
+                            r.start = pe;
+                            r.count = wc + gc - uint32_t(cut);
+                            r.nmeta = nn;
+                            r.raw = rr;
+                            r.pre = wc;
+                            r.cut = uint32_t(cut);
+                            mt = kResolved;
+                        }
+                    } else {
+#ifdef RAMCRC_WALK_DEBUG
+                        dbg_chase++;
+#endif
+                        // walked the whole part: its records go to the scratch
+                        // (C copies them), or, more than it holds, C walks it again
+                        jex = p;
+                        const bool keep = wc <= kPartRec && !huge;
+                        if (keep && uint32_t(lane) < wc)
+                            w.recs[pidx * kPartRec + uint32_t(lane)] = mine;
+                        if (lane == j) {
+                            r.start = pe;
+                            r.exit = p;
+                            r.count = wc;
+                            r.nmeta = wnn;
+                            r.raw = wrr;
+                            r.flags = keep ? wflags : (wflags | kPartChase);
+                            r.pre = r.cut = 0;
+                            mt = kResolved;
+                        }
+                    }
+                    if (wflags & kPartWrap)
+                        fallback = true;
+                } else {
 #ifdef RAMCRC_WALK_DEBUG
                     dbg_miss++;
 #endif
-                    xexit = x.exit;
-                    xcount = x.count;
-                    xflags = x.flags;
-                    if (lane == int(j)) {
-                        r.start = pos;
+                    // no guess: walk this part from the true offset, its
+                    // records to the scratch as above
+                    PartRes x;
+                    uint2 mine = make_uint2(0u, 0u);
+                    bool huge = false;
+                    walk_lane(w, tab, pe, stop, x,
+                              [&](uint32_t idx, uint32_t rp, uint32_t len, uint32_t hdr) {
+                                  if (uint32_t(lane) == idx)
+                                      mine = make_uint2(rp, (len << 8) | hdr);
+                                  huge = huge || len >= (1u << 24);
+                              },
+                              budget, wpeek);
+                    rewalk += x.count + 1;
+                    jex = x.exit;
+                    const bool keep = x.count <= kPartRec && !huge;
+                    if (keep && uint32_t(lane) < x.count)
+                        w.recs[(uint64_t(seg) * w.nparts + kj) * kPartRec + uint32_t(lane)] = mine;
+                    if (lane == j) {
+                        r.start = pe;
                         r.exit = x.exit;
                         r.count = x.count;
                         r.nmeta = x.nmeta;
                         r.raw = x.raw;
-                        r.flags = x.flags | kPartChase;
+                        r.flags = keep ? x.flags : (x.flags | kPartChase);
+                        r.pre = r.cut = 0;
+                        mt = kResolved;
                     }
+                    if (x.flags & kPartWrap)
+                        fallback = true;
                 }
-                if (xflags & kPartWrap) {
-                    fallback = true;
+                if (fallback)
                     break;
+                if (lane == j) {
+                    ok = true;
+                    emit = jemit;
+                    ex = jex;
+                    mt = kResolved;
                 }
-                if (lane == int(j)) {
-                    r.flags |= kPartEmit;
-                    r.rec = count;   // relative to the segment's first record
-                    if (st == pos && (fl & kPartWalked))
-                        r.pre = r.cut = 0;   // accepted as walked
+                // the part after j: its arrival offset is now known
+                if (lane == j + 1 && in) {
+                    mt = meet_at(k, gst, r.flags, r.count, jex, wr, wn);
+                    r.start = mt > 0 ? jex : gst;
+                    ok = mt >= 0;
+                    emit = ok;
                 }
-                count += xcount;
-                pos = xexit;
-                if (xflags & kPartOverrun)
-                    overrun = true;
             }
             if (fallback)
                 break;
-            fold(k < w.nparts && (r.flags & kPartEmit), r.nmeta, r.raw);
-            if (k < w.nparts)
+            // the chain ends at the first accepted part that overran
+            const uint64_t ovr = __ballot(emit && (r.flags & kPartOverrun));
+            const int olane = ovr ? int(__builtin_ctzll(ovr)) : kWaveSize;
+            if (lane > olane)
+                emit = false;
+            if (emit && mt > 0) {
+                // drop the guess's first `cut` entries (junk), whose header +
+                // length bytes are rebuilt from the records, and put the
+                // `hops` entries walked from the arrival offset in front
+#ifdef RAMCRC_WALK_DEBUG
+                dbg_meet++;
+#endif
+                const uint32_t hops = uint32_t(mt) >> 8, cut = uint32_t(mt) & 0xFF;
+                const uint64_t base = (uint64_t(seg) * w.nparts + k) * kPartRec;
+                uint32_t jr = 0, jn = 0;
+                for (uint32_t e = 0; e < cut; e++) {
+                    const uint2 g = w.recs[base + e];
+                    const uint32_t mb = ((g.y >> 6) & 3) + 2;
+                    const uint64_t qe = uint64_t(g.y & 0xFF) | (uint64_t(g.y >> 8) << 8);
+                    jr = meta_update(tab, jr, qe, mb);
+                    jn += mb;
+                }
+                const uint32_t tn = r.nmeta - jn;
+                const uint32_t tr = r.raw ^ mulmod_horner(jr, xpow8_dev(tn));
+                r.raw = mulmod_horner(wr, xpow8_dev(tn)) ^ tr;
+                r.nmeta = wn + tn;
+                r.count = hops + r.count - cut;
+                r.pre = hops;   // walked again (and emitted) by C
+                r.cut = cut;
+            } else if (emit && mt == 0) {
+                r.pre = r.cut = 0;   // accepted as walked
+            }
+            const uint32_t c = emit ? r.count : 0u;
+            uint32_t incl = c;   // inclusive prefix of the record counts
+#pragma unroll
+            for (int s = 1; s < kWaveSize; s <<= 1) {
+                const uint32_t y = __shfl_up(incl, s, kWaveSize);
+                if (lane >= s)
+                    incl += y;
+            }
+            fold(emit, r.nmeta, r.raw);
+            if (emit) {
+                r.rec = count + incl - c;
+                r.flags |= kPartEmit;
                 parts[k] = r;
+            }
+            count += uint32_t(__builtin_amdgcn_readlane(int(incl), kWaveSize - 1));
+            // the chain's position after the chunk: the overrun part's exit,
+            // else the last live part's
+            const int last = olane < kWaveSize ? olane
+                                               : int(nlive - 1 - k0 < uint32_t(kWaveSize - 1)
+                                                         ? nlive - 1 - k0 : uint32_t(kWaveSize - 1));
+            pos = uint32_t(__builtin_amdgcn_readlane(int(ex), last));
+            overrun = olane < kWaveSize;
         }
 #ifdef RAMCRC_WALK_DEBUG
         const uint64_t dbg_t1 = __builtin_amdgcn_s_memrealtime();
