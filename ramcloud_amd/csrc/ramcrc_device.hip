@@ -2809,6 +2809,7 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
                     uint32_t p = pe, wc = 0, wnn = 0, wrr = 0, wflags = kPartWalked;
                     int cut = -1;
                     uint2 mine = make_uint2(0u, 0u);   // record wc of the walk, in lane wc
+                    uint64_t mq = 0;                   // its header + length bytes
                     bool huge = false;
                     while (true) {
                         const uint64_t hit = __ballot(uint32_t(lane) < gn && g.x == p);
@@ -2824,8 +2825,12 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
                         }
                         const uint64_t q = wpeek(p);
                         const Hop h = hop_of(q, p);
-                        wrr = meta_update(tab, wrr, q, h.mbytes);
-                        wnn += h.mbytes;
+                        if (uint32_t(lane) == wc)
+                            mq = q;
+                        if (wc >= kWaveSize) {   // the first 64 are summed after the walk
+                            wrr = meta_update(tab, wrr, q, h.mbytes);
+                            wnn += h.mbytes;
+                        }
                         if (h.next > 0xFFFFFFFFull) {
                             wflags |= kPartWrap;
                             break;
@@ -2841,6 +2846,32 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
                         p = uint32_t(h.next);
                     }
                     rewalk += wc + 1;
+                    {
+                        // the header + length bytes of the walk's first 64 entries
+                        // (an entry that overran or wrapped included: the reference
+                        // checksums its header too), off the chase: each lane the
+                        // raw CRC of its entry's bytes moved past the later ones'
+                        // (suffix sums), XORed over the wave; then the entries after
+                        // the 64th, summed on the way
+                        const uint32_t seen = wc + ((wflags & (kPartWrap | kPartOverrun)) ? 1u : 0u);
+                        const bool inr = uint32_t(lane) < (seen < kWaveSize ? seen : uint32_t(kWaveSize));
+                        const uint32_t mb = inr ? uint32_t((mq >> 6) & 3) + 2 : 0u;
+                        const uint32_t re = inr ? meta_update(tab, 0u, mq, mb) : 0u;
+                        uint32_t incl = mb;
+#pragma unroll
+                        for (int s2 = 1; s2 < kWaveSize; s2 <<= 1) {
+                            const uint32_t y = __shfl_down(incl, s2, kWaveSize);
+                            if (lane + s2 < kWaveSize)
+                                incl += y;
+                        }
+                        const uint32_t hn = __shfl(incl, 0, kWaveSize);
+                        uint32_t hr = inr ? mulmod_horner(re, xpow8_dev(incl - mb)) : 0u;
+#pragma unroll
+                        for (int s2 = 1; s2 < kWaveSize; s2 <<= 1)
+                            hr ^= __shfl_xor(hr, s2, kWaveSize);
+                        wrr = mulmod_horner(hr, xpow8_dev(wnn)) ^ wrr;
+                        wnn += hn;
+                    }
                     if (cut >= 0 && (fl & kPartWrap)) {
                         wflags |= kPartWrap;   // met a chain that wraps: the serial walker
                     } else if (cut >= 0) {
