@@ -72,8 +72,11 @@ VARIANTS = {
     # parallel-walk sync search (k_walk_sync)
     "walkdbg": ["RAMCRC_WALK_DEBUG=1"],
     "fw32": ["RAMCRC_FIX_WIN_KIB=32"],
-    "fw8": ["RAMCRC_FIX_WIN_KIB=8"],
+    "sh4": ["RAMCRC_SYNC_HOPS=4"],
     "sh5": ["RAMCRC_SYNC_HOPS=5"],
+    "sh3": ["RAMCRC_SYNC_HOPS=3"],
+    "sh4_ss6": ["RAMCRC_SYNC_HOPS=4", "RAMCRC_SYNC_STAGE_KIB=6"],
+    "sh3_ss4": ["RAMCRC_SYNC_HOPS=3", "RAMCRC_SYNC_STAGE_KIB=4"],
     "sh7": ["RAMCRC_SYNC_HOPS=7"],
     "sh8": ["RAMCRC_SYNC_HOPS=8"],
     "sh10": ["RAMCRC_SYNC_HOPS=10"],
