@@ -280,3 +280,53 @@ def tombstone_segments(oracle, nseg, cap, seed=99):
         _, ck, _, _ = oracle.check_metadata(s, pos, 0)
         certs[i] = (pos, ck)
     return buf, certs, counts
+
+
+def mixed_segments(oracle, nseg, cap, seed=4242, fill=0.97):
+    """nseg segments of log entries with random sizes and types: objects of
+    24 B .. 200 KiB (tiny, 100 B-ish, 1 and 4 KiB, tens of KiB and larger
+    than a 64 KiB part of the parallel walk), tombstones and safe versions,
+    all payload bytes random (junk headers everywhere for the walk's
+    synchronisation).  Entries fill `fill` of the capacity; the certificate
+    matches the metadata.  Returns (buf, certs, counts)."""
+    rng = np.random.default_rng(seed)
+    buf = np.zeros(nseg * cap, np.uint8)
+    certs = np.zeros((nseg, 2), np.uint32)
+    counts = np.zeros(nseg, np.uint32)
+    kinds = np.array([0, 1, 2, 3, 4, 5, 6])
+    regimes = [np.array([0.20, 0.30, 0.20, 0.14, 0.08, 0.02, 0.06]),   # everything
+               np.array([0.40, 0.45, 0.05, 0.02, 0.00, 0.00, 0.08]),   # dense small entries
+               np.array([0.05, 0.10, 0.40, 0.40, 0.03, 0.00, 0.02]),   # 1-4 KiB objects
+               np.array([0.10, 0.10, 0.05, 0.05, 0.30, 0.35, 0.05])]   # large entries
+    for i in range(nseg):
+        probs = regimes[i % len(regimes)]
+        s = _seg(buf, i, cap)
+        parts = []
+        pos = 0
+        while True:
+            k = int(rng.choice(kinds, p=probs))
+            if k == 0:
+                n, t = int(rng.integers(24, 64)), segments.LOG_ENTRY_TYPE_OBJ
+            elif k == 1:
+                n, t = int(rng.integers(64, 200)), segments.LOG_ENTRY_TYPE_OBJ
+            elif k == 2:
+                n, t = int(rng.integers(900, 1200)), segments.LOG_ENTRY_TYPE_OBJ
+            elif k == 3:
+                n, t = int(rng.integers(3500, 4700)), segments.LOG_ENTRY_TYPE_OBJ
+            elif k == 4:
+                n, t = int(rng.integers(10000, 60000)), segments.LOG_ENTRY_TYPE_OBJ
+            elif k == 5:
+                n, t = int(rng.integers(70000, 200000)), segments.LOG_ENTRY_TYPE_OBJ
+            else:
+                n, t = int(rng.integers(32, 80)), int(rng.choice([segments.LOG_ENTRY_TYPE_OBJTOMB, 9]))
+            e = _log_entry(t, rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+            if pos + len(e) > int(cap * fill):
+                break
+            parts.append(e)
+            pos += len(e)
+        blob = b"".join(parts)
+        s[:len(blob)] = np.frombuffer(blob, np.uint8)
+        counts[i] = len(parts)
+        _, ck, _, _ = oracle.check_metadata(s, pos, 0, capacity=cap, table_cap=cap + 1)
+        certs[i] = (pos, ck)
+    return buf, certs, counts

@@ -178,6 +178,42 @@ def test_parallel_walk_8mib_vs_oracle(ramcrc, oracle_mod, value_len):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("seed", [4242, 77])
+def test_parallel_walk_mixed_sizes_vs_oracle(ramcrc, oracle_mod, seed):
+    """8 MiB segments of random-size entries (objects of 24 B .. 200 KiB,
+    tombstones, prepared-op tombstones) with random payloads: junk headers
+    everywhere, parts holding hundreds of entries (their records spill), parts
+    inside an entry (jumped over), guesses that meet the chain after a few
+    entries or never.  One segment gets a damaged length in its middle.
+    Status, records and object CRCs equal the oracle's, with both walkers."""
+    import torch
+    cap, nseg = 8 << 20, 6
+    buf, certs, counts = segment_cases.mixed_segments(oracle_mod, nseg, cap, seed=seed)
+    # segment 3: an entry near the middle claims 5 bytes more (the chain derails)
+    s3 = buf[3 * cap:4 * cap]
+    _, _, _, t3 = oracle_mod.check_metadata(s3, int(certs[3, 0]), int(certs[3, 1]), segment=3,
+                                            capacity=cap, table_cap=cap + 1)
+    mid = int(t3[len(t3) // 2, 1])
+    lbx = (int(s3[mid]) >> 6) + 1
+    ln = int.from_bytes(bytes(s3[mid + 1:mid + 1 + lbx]), "little") + 5
+    s3[mid + 1:mid + 1 + lbx] = np.frombuffer(ln.to_bytes(4, "little")[:lbx], np.uint8)
+    exp_status, exp_table, exp_crc = segment_cases.oracle_walk(oracle_mod, buf, certs, nseg, cap=cap)
+    for serial in (False, True):
+        status, n, table, crc = _run(ramcrc, buf, certs, nseg, cap, int(counts.sum()) * 2 + 4096,
+                                     serial)
+        assert np.array_equal(status, exp_status), (serial, status, exp_status)
+        assert n == exp_table.shape[0]
+        t_dev, c_dev = _sorted(table, crc)
+        t_exp, c_exp = _sorted(exp_table, exp_crc)
+        assert np.array_equal(t_dev, t_exp)
+        ok_seg = (exp_status[:, 0] & segments.SEG_OK) != 0
+        live = ((t_exp[:, 3] & 0x13F) == segments.LOG_ENTRY_TYPE_OBJ) & (t_exp[:, 2] >= 24) & ok_seg[t_exp[:, 0]]
+        assert np.array_equal(c_dev[live], c_exp[live])
+    assert (exp_status[[0, 1, 2, 4, 5], 0] & segments.SEG_OK).all()
+    torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
 def test_walk_verify_replay_mix(ramcrc, oracle_mod, golden):
     """Tombstones (src/ObjectManager.cc:752-758), safe versions (:873-880) and
     the transaction records (prepared ops and their tombstones, decision
