@@ -21,13 +21,47 @@
 #include <stdint.h>
 
 #include "Buffer.h"
+#if defined(__has_include)
+#if __has_include("Exception.h")
+#include "Exception.h"   // as the reference header does (src/Crc32C.h:22)
+#endif
+#endif
 #include "ramcrc.h"
 
 #ifndef PRIVATE
 #define PRIVATE private
 #endif
 
+/// The software path's lookup tables under the reference's names
+/// (src/Crc32C.h:25-34): references into libramcrc's compile-time tables
+/// (ramcrc_slice8_tables), indexed exactly like the reference's arrays.
+namespace Crc32CSlicingBy8 {
+extern const uint32_t (&crc_tableil8_o32)[256];
+extern const uint32_t (&crc_tableil8_o40)[256];
+extern const uint32_t (&crc_tableil8_o48)[256];
+extern const uint32_t (&crc_tableil8_o56)[256];
+extern const uint32_t (&crc_tableil8_o64)[256];
+extern const uint32_t (&crc_tableil8_o72)[256];
+extern const uint32_t (&crc_tableil8_o80)[256];
+extern const uint32_t (&crc_tableil8_o88)[256];
+}  // namespace Crc32CSlicingBy8
+
 namespace RAMCloud {
+
+/// The hardware CRC step of src/Crc32C.h:39-93: state in, state out, no
+/// inversion (SSE4.2 crc32 with three interleaved chains in libramcrc).
+static inline uint32_t
+intelCrc32C(uint32_t crc, const void* buffer, uint64_t bytes)
+{
+    return ramcrc_update_hw(crc, buffer, bytes);
+}
+
+/// The table-driven CRC step of src/Crc32C.h:96-153 (slicing-by-8).
+static inline uint32_t
+softwareCrc32C(uint32_t crc, const void* data, uint64_t length)
+{
+    return ramcrc_update_sw(crc, data, length);
+}
 
 /**
  * CRC32C (Castagnoli polynomial, as used by iSCSI) accumulated over any

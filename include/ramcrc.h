@@ -67,6 +67,13 @@ uint32_t ramcrc_update(uint32_t state, const void* data, uint64_t nbytes);
  * 1 if this CPU and build support the crc32 instruction. */
 int ramcrc_cpu_has_hw(void);
 
+/* The eight slicing-by-8 tables ramcrc_update_sw uses, 8 x 256 words, table k
+ * first: the values of the reference's Crc32CSlicingBy8::crc_tableil8_o32 ..
+ * crc_tableil8_o88 (src/Crc32C.h:25-34, src/Crc32C.cc:108-537), generated from
+ * the polynomial at compile time.  The drop-in header exposes them under the
+ * reference's names. */
+const uint32_t* ramcrc_slice8_tables(void);
+
 /* State algebra.  ramcrc_shift(s, n) is the
  * state reached from s by updating with n zero bytes; ramcrc_combine(a, b, n)
  * = raw state of A||B given a = raw(0-based) state after A and b = raw(0, B)

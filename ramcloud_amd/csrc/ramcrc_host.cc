@@ -150,6 +150,8 @@ uint32_t ramcrc_update(uint32_t state, const void* data, uint64_t nbytes)
 
 int ramcrc_cpu_has_hw(void) { return g_have_hw ? 1 : 0; }
 
+const uint32_t* ramcrc_slice8_tables(void) { return &kSlice.t[0][0]; }
+
 uint32_t ramcrc_shift(uint32_t state, uint64_t nbytes)
 {
     return ramcrc::mulmod(state, ramcrc::xpow8(nbytes));

@@ -166,6 +166,48 @@ static void run(const Vectors& v, bool forceSoftware)
     }
 }
 
+// The free functions and table names of the reference header
+// (src/Crc32C.h:25-34,39-153): intelCrc32C / softwareCrc32C agree with the
+// class on every known-answer prefix, and a slicing-by-8 written against the
+// Crc32CSlicingBy8 names (byte j of an 8-byte block through the table of its
+// distance 7 - j from the block end: o88 for byte 0 .. o32 for byte 7) gives
+// the same states -- so each name holds the table the reference's does.
+static uint32_t
+slicing8(uint32_t crc, const uint8_t* p, size_t n)
+{
+    using namespace Crc32CSlicingBy8;
+    for (; n >= 8; n -= 8, p += 8) {
+        const uint32_t x = crc ^ (uint32_t(p[0]) | uint32_t(p[1]) << 8 | uint32_t(p[2]) << 16 |
+                                  uint32_t(p[3]) << 24);
+        crc = crc_tableil8_o88[x & 0xFF] ^ crc_tableil8_o80[(x >> 8) & 0xFF] ^
+              crc_tableil8_o72[(x >> 16) & 0xFF] ^ crc_tableil8_o64[x >> 24] ^
+              crc_tableil8_o56[p[4]] ^ crc_tableil8_o48[p[5]] ^ crc_tableil8_o40[p[6]] ^
+              crc_tableil8_o32[p[7]];
+    }
+    for (; n; n--, p++)
+        crc = crc_tableil8_o32[(crc ^ *p) & 0xFF] ^ (crc >> 8);
+    return crc;
+}
+
+static void
+free_functions(const Vectors& v)
+{
+    const uint8_t* in = reinterpret_cast<const uint8_t*>(v.input.data());
+    for (size_t i = 0; i <= v.input.size(); i++) {
+        EXPECT_EQ(v.crcByLength[i], ~RAMCloud::intelCrc32C(0xFFFFFFFFu, in, i));
+        EXPECT_EQ(v.crcByLength[i], ~RAMCloud::softwareCrc32C(0xFFFFFFFFu, in, i));
+        EXPECT_EQ(v.crcByLength[i], ~slicing8(0xFFFFFFFFu, in, i));
+    }
+    std::vector<uint8_t> big(4099);
+    for (size_t i = 0; i < big.size(); i++)
+        big[i] = static_cast<uint8_t>((i * 40503u) >> 5);
+    for (size_t off = 0; off < 8; off++) {
+        const uint32_t s = static_cast<uint32_t>(0x9E3779B9u * (off + 1));
+        EXPECT_EQ(RAMCloud::intelCrc32C(s, big.data() + off, big.size() - off),
+                  slicing8(s, big.data() + off, big.size() - off));
+    }
+}
+
 int main(int argc, char** argv)
 {
     if (argc < 2) {
@@ -179,6 +221,7 @@ int main(int argc, char** argv)
     }
     run(v, false);
     run(v, true);
+    free_functions(v);
     printf("haveHardware=%d failures=%d\n", Crc32C::haveHardware ? 1 : 0, failures);
     return failures ? 1 : 0;
 }
