@@ -19,7 +19,7 @@ LIB = os.path.join(LIBDIR, "libramcrc.so")
 ARCH = "gfx950"
 
 SOURCES = ["ramcrc_device.hip", "ramcrc_host.cc", "ramcrc_shard.hip", "ramcrc_fill.hip"]
-HEADERS = ["gf2.h"]
+HEADERS = ["gf2.h", "walk_rules.h"]
 
 
 def hipcc():
@@ -72,6 +72,7 @@ VARIANTS = {
     # parallel-walk sync search (k_walk_sync)
     "walkdbg": ["RAMCRC_WALK_DEBUG=1"],
     "fw32": ["RAMCRC_FIX_WIN_KIB=32"],
+    "nocap": ["RAMCRC_NO_CAPTURE=1"],
     "sh4": ["RAMCRC_SYNC_HOPS=4"],
     "sh5": ["RAMCRC_SYNC_HOPS=5"],
     "sh3": ["RAMCRC_SYNC_HOPS=3"],

@@ -48,9 +48,12 @@
 #include <string.h>
 
 #include "gf2.h"
+#include "walk_rules.h"
 #include "ramcrc.h"
 
 namespace {
+
+using namespace ramcrc_walk;   // Hop, hop_of, plausible, first_hop4, kNumTypes
 
 using ramcrc::OpTable;
 
@@ -341,6 +344,16 @@ __device__ __forceinline__ const gu32x4* gptr16(uint64_t addr)
 
 __device__ __forceinline__ u32x4 load16(uint64_t addr) { return *gptr16(addr); }
 
+// The 4 bytes at a (any alignment; a + 8 rounded down to 4 stays inside the
+// buffer): two aligned dword loads and one byte funnel shift.
+__device__ __forceinline__ uint32_t load_u32_any(uint64_t a)
+{
+    typedef const __attribute__((address_space(1))) uint32_t g32;
+    const uint64_t b = a & ~uint64_t(3);
+    const uint32_t w0 = *reinterpret_cast<g32*>(b), w1 = *reinterpret_cast<g32*>(b + 4);
+    return __builtin_amdgcn_alignbyte(w1, w0, uint32_t(a) & 3);
+}
+
 // ------------------------------------------------------------ descriptors
 struct BatchDesc {
     const uint8_t* base;     // d_base
@@ -355,6 +368,9 @@ struct BatchDesc {
     const u32x4* rec;        // record mode: ramcrc_seg_entry table
     const uint64_t* n_dev;   // record mode: live entry count (device), <= n
     const u32x4* seg_status; // record mode: ramcrc_seg_status per segment (walk result)
+    ramcrc_seg_status* vstat; // record mode, nullable: k_entries compares each object's CRC
+                              // with its stored checksum (the 4 bytes before S, loaded beside
+                              // its head) and counts mismatches in vstat[segment].bad_objects
 };
 
 // Buffer addressing modes.
@@ -1144,7 +1160,9 @@ __device__ __forceinline__ void tiny_run(const BatchDesc& d, const Sorted& so, u
         return o;
     };
     // the group's eight windows: piece gl of each owner's 128-byte window
-    auto issue = [&](const TinyOwn& o, u32x4 (&w)[8], uint32_t (&geo)[8]) {
+    auto issue = [&](const TinyOwn& o, u32x4 (&w)[8], uint32_t (&geo)[8], uint32_t& st) {
+        // the owner's stored object checksum (records mode), beside its window
+        st = d.vstat && o.ix != kNoIdx ? load_u32_any(o.S - 4) : 0u;
         static_for8([&](auto qc) {
             constexpr int q = decltype(qc)::value;
             geo[q] = swz_from<q>(o.geo);
@@ -1162,14 +1180,14 @@ __device__ __forceinline__ void tiny_run(const BatchDesc& d, const Sorted& so, u
     __syncthreads();
     const uint32_t* tab = reinterpret_cast<const uint32_t*>(lds);
     u32x4 wc[8];
-    uint32_t gc[8];
-    issue(o0, wc, gc);
+    uint32_t gc[8], sc;
+    issue(o0, wc, gc, sc);
     for (; r < rounds; r += nwaves) {
         const TinyOwn o2 = load_own(r + 2 * nwaves);
         u32x4 wn[8];
-        uint32_t gn[8];
+        uint32_t gn[8], sn = 0;
         if (r + nwaves < rounds)
-            issue(o1, wn, gn);
+            issue(o1, wn, gn, sn);
         uint32_t mine = 0;
 #pragma unroll
         for (int q = 0; q < 8; q++) {
@@ -1210,10 +1228,14 @@ __device__ __forceinline__ void tiny_run(const BatchDesc& d, const Sorted& so, u
                 for (uint32_t k = 0; k < o0.len; k++)
                     R = tab[(1 + kTinyRow0) * 256 + ((R ^ *(const gu8*)(o0.S + k)) & 0xFF)] ^ (R >> 8);
             }
-            d.out[o0.ix] = finalize ? ~R : R;
+            const uint32_t Rf = finalize ? ~R : R;
+            d.out[o0.ix] = Rf;
+            if (d.vstat && Rf != sc)
+                atomicAdd(&d.vstat[d.rec[o0.ix].x].bad_objects, 1u);
         }
         o0 = o1;
         o1 = o2;
+        sc = sn;
 #pragma unroll
         for (int q = 0; q < 8; q++) {
             wc[q] = wn[q];
@@ -1261,18 +1283,22 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
     const uint64_t dummy = reinterpret_cast<uint64_t>(so.bt);   // device memory, 16 B aligned
 
     // batched unpad: lane gl holds octet gl of the current batch of eight
-    uint32_t bY = 0, bPad = 0, bIx = kNoIdx;
+    uint32_t bY = 0, bPad = 0, bIx = kNoIdx, bSt = 0;
     int nb = 0;
     auto flush_batch = [&]() {
         const uint32_t R = mulmod_horner(bY, xinv[bPad & 127]);
-        if (bIx != kNoIdx)
-            d.out[bIx] = finalize ? ~R : R;
+        if (bIx != kNoIdx) {
+            const uint32_t Rf = finalize ? ~R : R;
+            d.out[bIx] = Rf;
+            if (d.vstat && Rf != bSt)   // ObjectManager::replaySegment's check (:659-663)
+                atomicAdd(&d.vstat[d.rec[bIx].x].bad_objects, 1u);
+        }
         bIx = kNoIdx;
         nb = 0;
     };
     // deferred fold of the previous octet
     bool pend = false;
-    uint32_t pu0 = 0, pu1 = 0, pu2 = 0, pu3 = 0, ppad = 0, pix = kNoIdx;
+    uint32_t pu0 = 0, pu1 = 0, pu2 = 0, pu3 = 0, ppad = 0, pix = kNoIdx, pst = 0;
     auto flush = [&]() {
         if (pend) {
             const uint32_t Y = group_fold(lds, gl, pu0, pu1, pu2, pu3);
@@ -1280,6 +1306,7 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
                 bY = Y;
                 bPad = ppad;
                 bIx = pix;
+                bSt = pst;
             }
             pend = false;
             if (++nb == kG)
@@ -1306,7 +1333,7 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
             const uint32_t K = uint32_t(b);
             struct Oct {
                 uint64_t S, E;
-                uint32_t init, ix, steps;
+                uint32_t init, ix, steps, st;
                 u32x4 w[kSmallK + 1];
             };
             auto load_oct = [&](uint64_t o, Oct& t) {
@@ -1320,6 +1347,7 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
                 const uint64_t A = line_base(t.S);
                 const uint64_t p0 = A + gl * 16;
                 const uint64_t safe = t.steps ? A : dummy;
+                t.st = d.vstat && t.steps ? load_u32_any(t.S - 4) : 0u;
 #pragma unroll
                 for (int k = 0; k <= kSmallK; k++) {
                     const uint64_t a = p0 + uint64_t(k) * kStep;
@@ -1374,6 +1402,7 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
                 pu3 = u3;
                 ppad = uint32_t((A + uint64_t(cur.steps) * kStep) - cur.E);
                 pix = cur.ix;
+                pst = cur.st;
                 flush();
                 cur = nxt;
             }
@@ -1427,6 +1456,9 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
 #pragma unroll
             for (int j = 0; j < kPU; j++)
                 Abuf[j] = ldf(1 + j < kt0 ? 1 + j : 0);
+            // the stored checksum (records mode) behind the data loads; read at
+            // the octet's end
+            const uint32_t stv = d.vstat && steps ? load_u32_any(S - 4) : 0u;
             __builtin_amdgcn_sched_barrier(0);
             flush();
 
@@ -1508,6 +1540,7 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
             pu3 = u3;
             ppad = uint32_t((A + uint64_t(steps) * kStep) - E);
             pix = ix;
+            pst = stv;
         }
         }
     }
@@ -2180,7 +2213,6 @@ constexpr uint32_t kSyncSpan = 16384;               // candidate bytes searched 
 constexpr uint32_t kMeetMax = 4;                    // B's fast path: meets within 4 records
 constexpr uint32_t kMeetHops = 3;                   // ... after at most 3 entries walked
 constexpr uint32_t kRewalkBudget = 1u << 15;        // hops B may re-walk before falling back
-constexpr uint32_t kNumTypes = 12;                  // TOTAL_LOG_ENTRY_TYPES, src/LogEntryTypes.h:68
 // part flags
 constexpr uint32_t kPartWalked = 1u, kPartWrap = 2u, kPartOverrun = 4u, kPartEmit = 8u;
 constexpr uint32_t kPartSpill = 16u;   // A: more records than its scratch holds
@@ -2231,25 +2263,6 @@ __device__ __forceinline__ uint64_t seg_peek(uint64_t seg, uint32_t pos, uint32_
     return ((uint64_t(w1) << 32) | w0) >> (8 * (pos & 3));
 }
 
-// One hop of the reference walk from a header read as q: the entry's metadata
-// byte count (1 + lengthBytes), payload length and the next offset (64-bit,
-// so that a uint32_t wrap is visible).
-struct Hop {
-    uint32_t mbytes, len;
-    uint64_t next;
-};
-
-__device__ __forceinline__ Hop hop_of(uint64_t q, uint32_t pos)
-{
-    const uint32_t t = (uint32_t(q) >> 6) & 3;   // getLengthBytes() - 1
-    const uint64_t mask = t == 3 ? 0xFFFFFFFFull : ((1ull << (8 * (t + 1))) - 1);
-    Hop h;
-    h.len = uint32_t((q >> 8) & mask);
-    h.mbytes = t + 2;
-    h.next = uint64_t(pos) + h.mbytes + h.len;
-    return h;
-}
-
 // raw CRC update by an entry's header + length bytes (2..5 of them, from q).
 __device__ __forceinline__ uint32_t meta_update(const uint32_t* tab, uint32_t c, uint64_t q,
                                                 uint32_t mbytes)
@@ -2285,37 +2298,6 @@ __device__ __forceinline__ uint32_t walk_limit(const PWalk& w, uint64_t seg)
 constexpr uint32_t kSyncStage = RAMCRC_SYNC_STAGE_KIB * 1024;   // staged bytes per wave
 constexpr uint32_t kSyncWin = kSyncStage - 16;       // candidates / hops read from LDS below this
 constexpr int kSyncWaves = 4;                        // waves per workgroup
-
-// A hop a candidate chain may take: a header of a type the log writes
-// (src/LogEntryTypes.h:29-68: 1 .. TOTAL-1; INVALID = 0 only fills the
-// zeroed tail), length bytes in the canonical (shortest) form EntryHeader
-// writes (src/Segment.h:135-148), and an entry that ends inside the segment.
-__device__ __forceinline__ bool plausible(uint64_t q, const Hop& h, uint32_t capacity)
-{
-    const uint32_t type = uint32_t(q) & 0x3f;
-    const uint32_t t = h.mbytes - 2;   // lengthBytes - 1
-    const bool canon = t == 0 || ((h.len >> (8 * t)) != 0);
-    return type != 0 && type < kNumTypes && canon && h.next <= capacity;
-}
-
-// First-hop filter of four candidates at once (bytes of h, one candidate
-// per byte; top3 = for each, the byte three further on, the top length byte
-// of a 3-byte length): a superset of plausible() -- the type is 1..11, and,
-// where the capacity rules them out, no 4-byte length (>= 2^24 when
-// canonical) and no 3-byte length with its top bit set (>= 2^23).  Returns
-// one bit per candidate.
-__device__ __forceinline__ uint32_t first_hop4(uint32_t h, uint32_t top3, bool kill4, bool kill3)
-{
-    const uint32_t t = h & 0x3f3f3f3fu;
-    constexpr uint32_t kLo = 0x3f3f3f3fu;                      // t + 63 >= 64 iff t >= 1
-    constexpr uint32_t kHi = 0x01010101u * (64 - kNumTypes);    // t + 52 >= 64 iff t >= 12
-    uint32_t ok = ((t + kLo) & ~(t + kHi) & 0x40404040u) << 1;   // bit 7 of each byte
-    const uint32_t lb4 = h & (h << 1) & 0x80808080u;
-    const uint32_t lb3 = h & ~(h << 1) & 0x80808080u;
-    ok &= ~((kill4 ? lb4 : 0u) | (kill3 ? (lb3 & top3) : 0u));
-    const uint32_t x = ok >> 7;
-    return (x | (x >> 7) | (x >> 14) | (x >> 21)) & 0xFu;
-}
 
 // Wave minimum through DPP (quad swaps, half-row and row mirrors, row
 // broadcasts): the result is valid in lane 63 and returned uniform.
@@ -3235,6 +3217,8 @@ __global__ __launch_bounds__(256) void k_obj_compare(BatchDesc d, ramcrc_seg_sta
     if (hdr == 0)
         return;
     const bool readable = r.z >= hdr && !(r.w & kRecOverlong);
+    if (d.vstat && type == RAMCRC_LOG_ENTRY_TYPE_OBJ && readable && !is_large(uint64_t(r.z) - 4))
+        return;   // compared by k_entries beside its scan (objects below the 64 KiB split)
     const uint64_t payload = reinterpret_cast<uint64_t>(d.base) + uint64_t(r.x) * d.seg_bytes +
                              r.y + 1 + ((r.w >> 6) & 3) + 1;
     const gu8* p = reinterpret_cast<const gu8*>(payload);
@@ -3890,6 +3874,9 @@ int ramcrc_verify_objects_device(ramcrc_ctx* c, const void* d_base, uint64_t seg
     d.base = static_cast<const uint8_t*>(d_base);
     d.seg_bytes = seg_stride;
     d.n = entries_cap;
+#ifndef RAMCRC_NO_CAPTURE
+    d.vstat = d_status;
+#endif
     d.rec = reinterpret_cast<const u32x4*>(d_entries);
     d.n_dev = d_n_entries;
     d.seg_status = reinterpret_cast<const u32x4*>(d_status);
