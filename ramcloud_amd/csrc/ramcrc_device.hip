@@ -1176,12 +1176,14 @@ __device__ __forceinline__ void tiny_run(const BatchDesc& d, const Sorted& so, u
 
     uint64_t r = wave;
     TinyOwn o0 = load_own(r), o1 = load_own(r + nwaves);
+    // (issuing the first round's windows before the table fill was 1-2 %
+    // slower: the fill's loads queue behind them)
     fill_plain(lds, 0, &g_tab.pos[0][0], 132 * 256);
     __syncthreads();
-    const uint32_t* tab = reinterpret_cast<const uint32_t*>(lds);
     u32x4 wc[8];
     uint32_t gc[8], sc;
     issue(o0, wc, gc, sc);
+    const uint32_t* tab = reinterpret_cast<const uint32_t*>(lds);
     for (; r < rounds; r += nwaves) {
         const TinyOwn o2 = load_own(r + 2 * nwaves);
         u32x4 wn[8];
