@@ -73,6 +73,7 @@ VARIANTS = {
     "walkdbg": ["RAMCRC_WALK_DEBUG=1"],
     "fw32": ["RAMCRC_FIX_WIN_KIB=32"],
     "nocap": ["RAMCRC_NO_CAPTURE=1"],
+    "ew12": ["RAMCRC_ENT_WAVES=12"],
     "sh4": ["RAMCRC_SYNC_HOPS=4"],
     "sh5": ["RAMCRC_SYNC_HOPS=5"],
     "sh3": ["RAMCRC_SYNC_HOPS=3"],
