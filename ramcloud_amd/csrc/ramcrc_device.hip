@@ -2219,6 +2219,7 @@ constexpr uint32_t kRewalkBudget = 1u << 15;        // hops B may re-walk before
 constexpr uint32_t kPartWalked = 1u, kPartWrap = 2u, kPartOverrun = 4u, kPartEmit = 8u;
 constexpr uint32_t kPartSpill = 16u;   // A: more records than its scratch holds
 constexpr uint32_t kPartChase = 32u;   // B: walked again; C walks it once more
+constexpr uint32_t kPartHuge = 64u;    // A: an entry of 16 MiB or more (records hold 24-bit lengths)
 constexpr uint32_t kPartRec = 64;      // records A keeps per part (C copies them)
 
 struct PartRes {
@@ -2594,7 +2595,9 @@ __device__ __forceinline__ void walk_tab_fill(uint32_t* tab)
 // while it chases, then the wave writes them part by part with coalesced
 // stores: records stored by a lane one hop at a time would reach memory as
 // partial lines.  A part with more than kPartRec records, or an entry of
-// 16 MiB or more, is marked kPartSpill and walked again by C.
+// 16 MiB or more, is marked kPartSpill and walked again by C; its first
+// kPartRec records still go to the scratch (B meets a misguessed chain within
+// its first few entries), unless an entry's length does not fit a record.
 __global__ __launch_bounds__(256) void k_walk_parts(PWalk w)
 {
     __shared__ uint32_t tab[4 * 256];
@@ -2631,16 +2634,19 @@ __global__ __launch_bounds__(256) void k_walk_parts(PWalk w)
                       kPartBytes);
             if (r.count > kPartRec || spill)
                 r.flags |= kPartSpill;
+            if (spill)
+                r.flags |= kPartHuge;
         }
         w.parts[i] = r;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS records
-    const bool flush = valid && (r.flags & kPartWalked) && !(r.flags & kPartSpill);
+    const bool flush = valid && (r.flags & kPartWalked) && !(r.flags & kPartHuge);
     uint64_t todo = __ballot(flush);
     while (todo) {
         const int j = __builtin_ctzll(todo);
         todo &= todo - 1;
-        const uint32_t n = __shfl(r.count, j, kWaveSize);
+        uint32_t n = __shfl(r.count, j, kWaveSize);
+        n = n < kPartRec ? n : kPartRec;
         const uint64_t dst = (i - uint64_t(lane) + uint64_t(j)) * kPartRec;
         const uint2* src = lrec[(threadIdx.x & ~63u) + uint32_t(j)];
         for (uint32_t e = uint32_t(lane); e < n; e += kWaveSize)
@@ -2714,8 +2720,9 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
             const uint64_t Ek = (uint64_t(k) << kPartShift) + kPartBytes;
             if (!(fl & kPartWalked) || (fl & kPartWrap) || uint64_t(pe) >= Ek)
                 return -1;
-            // a spilled part's records are not in the scratch: met at its start only
-            const uint32_t gn = (fl & kPartSpill) ? 0u : (gc < kPartRec ? gc : kPartRec);
+            // the scratch holds a part's first kPartRec records (none when an
+            // entry's length does not fit a record): met at its start only then
+            const uint32_t gn = (fl & kPartHuge) ? 0u : (gc < kPartRec ? gc : kPartRec);
             const uint64_t base = (uint64_t(seg) * w.nparts + k) * kPartRec;
             uint32_t p = pe;
             for (uint32_t hh = 0;; hh++) {
@@ -2791,7 +2798,7 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
                     // are the true chain's.  Without a meeting the walk covers
                     // the part (a full re-walk).
                     const uint32_t gc = uint32_t(__builtin_amdgcn_readlane(int(r.count), j));
-                    const uint32_t gn = (fl & kPartSpill) ? 0u : (gc < kPartRec ? gc : kPartRec);
+                    const uint32_t gn = (fl & kPartHuge) ? 0u : (gc < kPartRec ? gc : kPartRec);
                     const uint64_t pidx = uint64_t(seg) * w.nparts + kj;
                     uint2 g = make_uint2(0xFFFFFFFFu, 0u);
                     if (uint32_t(lane) < gn)
