@@ -185,8 +185,8 @@ typedef struct ramcrc_seg_status {
 /* Segment::checkMetadataIntegrity (src/Segment.cc:758-800) for n_seg segments
  * at d_base + i*seg_stride, each of seg_capacity bytes (a multiple of 16; the
  * reference's segletBlocks.size() * segletSize), against d_certs[i].  The
- * length-prefixed entries are walked in parallel over 64 KiB parts of every
- * segment (see RAMCRC_OPT_SERIAL_WALK).  Writes d_status[i] and one
+ * length-prefixed entries are walked in parallel over parts of every segment
+ * (64 KiB by default; see RAMCRC_OPT_SERIAL_WALK, RAMCRC_OPT_WALK_PART_SHIFT).  Writes d_status[i] and one
  * ramcrc_seg_entry per complete entry to d_entries (up to entries_cap; the
  * order across segments is unspecified, within a segment it is increasing).  *d_n_entries (device) receives the
  * number of entries walked (may exceed entries_cap: see TABLE_FULL).
@@ -354,6 +354,12 @@ int ramcrc_assemble_objects_host(ramcrc_ctx* ctx, void* const* objs, const uint6
  *                           (offset wraps) to the serial walker.  Both give
  *                           identical results. */
 #define RAMCRC_OPT_SERIAL_WALK 1
+/*   RAMCRC_OPT_WALK_PART_SHIFT  log2 of the parallel walk's part size, 13..20
+ *                           (8 KiB .. 1 MiB); 0: the default, 64 KiB.
+ *                           Results are identical for every part size (the
+ *                           parity tests run several); smaller parts measured
+ *                           no faster even on segments of 100-byte entries. */
+#define RAMCRC_OPT_WALK_PART_SHIFT 2
 int ramcrc_ctx_set_option(ramcrc_ctx* ctx, int option, int64_t value);
 
 /* Kernel timing (for benchmarks): when enabled, every launch brackets its

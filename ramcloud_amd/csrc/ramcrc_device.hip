@@ -1728,6 +1728,7 @@ struct ramcrc_ctx {
     void* walk_recs = nullptr;
     uint64_t walk_recs_cap = 0;
     bool serial_walk = false;   // RAMCRC_OPT_SERIAL_WALK
+    uint32_t walk_pshift = 0;   // RAMCRC_OPT_WALK_PART_SHIFT; 0: kPartShift
     // benchmark timing of the scan kernels
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_used, ev_free;
@@ -2195,8 +2196,8 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
 #ifndef RAMCRC_PART_SHIFT
 #define RAMCRC_PART_SHIFT 16
 #endif
-constexpr uint32_t kPartShift = RAMCRC_PART_SHIFT;  // 64 KiB parts
-constexpr uint32_t kPartBytes = 1u << kPartShift;
+constexpr uint32_t kPartShift = RAMCRC_PART_SHIFT;  // default parts: 64 KiB
+constexpr uint32_t kPartShiftMin = 13;               // smallest part (RAMCRC_OPT_WALK_PART_SHIFT)
 constexpr uint32_t kNoStart = 0xFFFFFFFFu;
 #ifndef RAMCRC_SYNC_HOPS
 #define RAMCRC_SYNC_HOPS 6
@@ -2249,6 +2250,7 @@ struct PWalk {
     uint32_t* fallback;   // per segment: nonzero = walked by k_seg_walk
     uint64_t* seg_base;   // per segment: first record slot (B)
     uint2* recs;          // per part: kPartRec records of A's walk {offset, length << 8 | header}
+    uint32_t pshift;      // log2 part bytes of this launch
 };
 
 typedef const __attribute__((address_space(1))) uint32_t gu32;
@@ -2330,11 +2332,11 @@ __global__ __launch_bounds__(kSyncWaves * kWaveSize) void k_walk_sync(PWalk w)
         const uint32_t k = uint32_t(i - seg * w.nparts);
         if (k == 0)
             continue;   // part 0 starts at offset 0
-        const uint32_t B = k << kPartShift;
+        const uint32_t B = k << w.pshift;
         const uint32_t limit = walk_limit(w, seg);
         const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
         uint64_t end64 = uint64_t(B) + kSyncSpan;
-        end64 = end64 < uint64_t(B) + kPartBytes ? end64 : uint64_t(B) + kPartBytes;
+        end64 = end64 < uint64_t(B) + (1ull << w.pshift) ? end64 : uint64_t(B) + (1ull << w.pshift);
         end64 = end64 < w.capacity ? end64 : w.capacity;
         const uint32_t end = uint32_t(end64 < limit ? end64 : limit);
         if (end <= B) {
@@ -2612,7 +2614,7 @@ __global__ __launch_bounds__(256) void k_walk_parts(PWalk w)
     if (valid) {
         const uint64_t seg = i / w.nparts;
         const uint32_t k = uint32_t(i - seg * w.nparts);
-        const uint32_t B = k << kPartShift;
+        const uint32_t B = k << w.pshift;
         const uint32_t limit = walk_limit(w, seg);
         r = w.parts[i];
         const uint32_t start = k == 0 ? 0u : r.start;
@@ -2622,8 +2624,8 @@ __global__ __launch_bounds__(256) void k_walk_parts(PWalk w)
             r.count = r.nmeta = r.raw = 0;
             r.exit = start;
         } else {
-            const uint32_t pend = uint32_t(uint64_t(B) + kPartBytes < w.capacity
-                                               ? uint64_t(B) + kPartBytes : w.capacity);
+            const uint32_t pend = uint32_t(uint64_t(B) + (1ull << w.pshift) < w.capacity
+                                               ? uint64_t(B) + (1ull << w.pshift) : w.capacity);
             const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
             walk_lane(w, tab, seg, sb, start, pend < limit ? pend : limit, r,
                       [&](uint32_t idx, uint32_t pos, uint32_t len, uint32_t hdr) {
@@ -2631,7 +2633,7 @@ __global__ __launch_bounds__(256) void k_walk_parts(PWalk w)
                               mine[idx] = make_uint2(pos, (len << 8) | hdr);
                           spill = spill || len >= (1u << 24);
                       },
-                      kPartBytes);
+                      1u << w.pshift);
             if (r.count > kPartRec || spill)
                 r.flags |= kPartSpill;
             if (spill)
@@ -2717,7 +2719,7 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
         auto meet_at = [&](uint32_t k, uint32_t st, uint32_t fl, uint32_t gc, uint32_t pe,
                            uint32_t& wr, uint32_t& wn) -> int {
             wr = wn = 0;
-            const uint64_t Ek = (uint64_t(k) << kPartShift) + kPartBytes;
+            const uint64_t Ek = (uint64_t(k) << w.pshift) + (1ull << w.pshift);
             if (!(fl & kPartWalked) || (fl & kPartWrap) || uint64_t(pe) >= Ek)
                 return -1;
             // the scratch holds a part's first kPartRec records (none when an
@@ -2743,7 +2745,7 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
             }
         };
         const uint32_t nlive =
-            limit == 0 ? 0u : uint32_t((uint64_t(limit) + kPartBytes - 1) >> kPartShift);
+            limit == 0 ? 0u : uint32_t((uint64_t(limit) + (1ull << w.pshift) - 1) >> w.pshift);
         for (uint32_t k0 = 0; k0 < nlive && !overrun && !fallback; k0 += kWaveSize) {
             const uint32_t k = k0 + uint32_t(lane);
             const bool in = k < nlive;
@@ -2783,7 +2785,7 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
                 const uint32_t pe = j == 0 ? pos : uint32_t(__builtin_amdgcn_readlane(int(ex), j - 1));
                 const uint32_t st = uint32_t(__builtin_amdgcn_readlane(int(gst), j));
                 const uint32_t fl = uint32_t(__builtin_amdgcn_readlane(int(r.flags), j));
-                const uint64_t Ej64 = (uint64_t(kj) << kPartShift) + kPartBytes;
+                const uint64_t Ej64 = (uint64_t(kj) << w.pshift) + (1ull << w.pshift);
                 const uint32_t Ej = uint32_t(Ej64 < w.capacity ? Ej64 : w.capacity);
                 const uint32_t stop = Ej < limit ? Ej : limit;
                 const uint32_t budget = rewalk < kRewalkBudget ? kRewalkBudget - rewalk : 0u;
@@ -3122,15 +3124,15 @@ __global__ __launch_bounds__(256) void k_walk_emit(PWalk w)
     const uint32_t pre = emit && !chase ? r.pre : 0u;
     if (chase || pre) {
         const uint32_t k = uint32_t(i - seg * w.nparts);
-        const uint32_t B = k << kPartShift;
+        const uint32_t B = k << w.pshift;
         const uint32_t limit = walk_limit(w, seg);
-        const uint32_t pend = uint32_t(uint64_t(B) + kPartBytes < w.capacity ? uint64_t(B) + kPartBytes
+        const uint32_t pend = uint32_t(uint64_t(B) + (1ull << w.pshift) < w.capacity ? uint64_t(B) + (1ull << w.pshift)
                                                                              : w.capacity);
         const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
         PartRes x;
         walk_lane(w, tab, seg, sb, r.start, pend < limit ? pend : limit, x,
                   TableSink{w.entries + slot, slot < w.cap ? w.cap - slot : 0, uint32_t(seg)},
-                  chase ? kPartBytes : pre);
+                  chase ? (1u << w.pshift) : pre);
     }
 }
 
@@ -3424,6 +3426,11 @@ int ramcrc_ctx_set_option(ramcrc_ctx* c, int option, int64_t value)
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     switch (option) {
     case RAMCRC_OPT_SERIAL_WALK: c->serial_walk = value != 0; return RAMCRC_OK;
+    case RAMCRC_OPT_WALK_PART_SHIFT:
+        if (value != 0 && (value < kPartShiftMin || value > 20))
+            return RAMCRC_EINVAL;
+        c->walk_pshift = uint32_t(value);
+        return RAMCRC_OK;
     default: return RAMCRC_EINVAL;
     }
 }
@@ -3811,7 +3818,11 @@ int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_s
         // parallel walk: sync search, part walks, per-segment fix-up, record
         // emission; the serial walker then takes only the segments the fix-up
         // handed back (uint32_t wraps, exhausted re-walk budget)
-        const uint32_t nparts = uint32_t((uint64_t(seg_capacity) + kPartBytes - 1) >> kPartShift);
+        // part size (RAMCRC_OPT_WALK_PART_SHIFT): smaller parts do not pay on
+        // dense segments -- A and C then read a cache line per entry header
+        // and are bound by those fetches, not by their chains
+        const uint32_t pshift = c->walk_pshift ? c->walk_pshift : kPartShift;
+        const uint32_t nparts = uint32_t((uint64_t(seg_capacity) + (1ull << pshift) - 1) >> pshift);
         const uint64_t total = n_seg * uint64_t(nparts);
         int rc = grow_device(&c->walk_parts, &c->walk_parts_cap, total, sizeof(PartRes));
         if (!rc)
@@ -3839,6 +3850,7 @@ int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_s
         pw.fallback = c->walk_fallback;
         pw.seg_base = c->walk_base;
         pw.recs = static_cast<uint2*>(c->walk_recs);
+        pw.pshift = pshift;
         if (nparts > 1) {
             uint64_t g0 = (total + kSyncWaves - 1) / kSyncWaves;
             if (g0 > uint64_t(8) * c->ncu)

@@ -263,6 +263,11 @@ class Context:
         the parallel walk (RAMCRC_OPT_SERIAL_WALK)."""
         _check(lib().ramcrc_ctx_set_option(self._h, 1, 1 if enable else 0), "ramcrc_ctx_set_option")
 
+    def set_walk_part_shift(self, shift):
+        """log2 of the parallel walk's part size, 13..20; 0 = the default 64 KiB
+        (RAMCRC_OPT_WALK_PART_SHIFT)."""
+        _check(lib().ramcrc_ctx_set_option(self._h, 2, int(shift)), "ramcrc_ctx_set_option")
+
     def set_cus(self, ncu):
         """Size this context's persistent grids for ncu CUs (0 = all): for
         launches on a CU-masked stream (see cu_mask_stream)."""

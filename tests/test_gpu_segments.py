@@ -16,12 +16,14 @@ def _sorted(table, extra=None):
     return table[order], (None if extra is None else extra[order])
 
 
-def _run(ramcrc, buf, certs, nseg, cap, entries_cap, serial=False):
+def _run(ramcrc, buf, certs, nseg, cap, entries_cap, serial=False, part_shift=0):
     import torch
 
     ctx = ramcrc.Context(0)
     if serial:
         ctx.set_serial_walk(True)
+    if part_shift:
+        ctx.set_walk_part_shift(part_shift)
     d = torch.from_numpy(buf).cuda()
     dc = torch.from_numpy(np.ascontiguousarray(certs).view(np.int32)).cuda()
     rv = segments.RecoveryVerify(ctx, nseg, cap, entries_cap=entries_cap)
@@ -161,9 +163,9 @@ def test_parallel_walk_8mib_vs_oracle(ramcrc, oracle_mod, value_len):
     certs[2, 1] ^= 0x10
     exp_status, exp_table, exp_crc = segment_cases.oracle_walk(oracle_mod, buf, certs, nseg, cap=cap)
     got = {}
-    for serial in (False, True):
+    for serial, shift in ((False, 0), (False, 13), (True, 0)):
         status, n, table, crc = _run(ramcrc, buf, certs, nseg, cap, int(counts.sum()) * 2 + 1024,
-                                     serial)
+                                     serial, shift)
         assert np.array_equal(status, exp_status), (serial, status, exp_status)
         assert n == exp_table.shape[0]
         t_dev, c_dev = _sorted(table, crc)
@@ -198,9 +200,9 @@ def test_parallel_walk_mixed_sizes_vs_oracle(ramcrc, oracle_mod, seed):
     ln = int.from_bytes(bytes(s3[mid + 1:mid + 1 + lbx]), "little") + 5
     s3[mid + 1:mid + 1 + lbx] = np.frombuffer(ln.to_bytes(4, "little")[:lbx], np.uint8)
     exp_status, exp_table, exp_crc = segment_cases.oracle_walk(oracle_mod, buf, certs, nseg, cap=cap)
-    for serial in (False, True):
+    for serial, shift in ((False, 0), (False, 13), (False, 14), (False, 17), (True, 0)):
         status, n, table, crc = _run(ramcrc, buf, certs, nseg, cap, int(counts.sum()) * 2 + 4096,
-                                     serial)
+                                     serial, shift)
         assert np.array_equal(status, exp_status), (serial, status, exp_status)
         assert n == exp_table.shape[0]
         t_dev, c_dev = _sorted(table, crc)
