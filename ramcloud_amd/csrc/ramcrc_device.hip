@@ -1727,6 +1727,14 @@ struct ramcrc_ctx {
     uint64_t walk_base_cap = 0;
     void* walk_recs = nullptr;
     uint64_t walk_recs_cap = 0;
+    void* walk_pool = nullptr;            // A's records past a part's first 64
+    uint64_t walk_pool_cap = 0;
+    uint32_t* walk_pool_owner = nullptr;
+    uint64_t walk_pool_owner_cap = 0;
+    uint32_t* walk_blocks = nullptr;
+    uint64_t walk_blocks_cap = 0;
+    unsigned long long* walk_pool_used = nullptr;
+    uint64_t walk_pool_used_cap = 0;
     bool serial_walk = false;   // RAMCRC_OPT_SERIAL_WALK
     uint32_t walk_pshift = 0;   // RAMCRC_OPT_WALK_PART_SHIFT; 0: kPartShift
     // benchmark timing of the scan kernels
@@ -2221,6 +2229,7 @@ constexpr uint32_t kPartWalked = 1u, kPartWrap = 2u, kPartOverrun = 4u, kPartEmi
 constexpr uint32_t kPartSpill = 16u;   // A: more records than its scratch holds
 constexpr uint32_t kPartChase = 32u;   // B: walked again; C walks it once more
 constexpr uint32_t kPartHuge = 64u;    // A: an entry of 16 MiB or more (records hold 24-bit lengths)
+constexpr uint32_t kMaxBlocks = 15;    // pool blocks per part: records 64 .. 1023 of A's walk
 constexpr uint32_t kPartRec = 64;      // records A keeps per part (C copies them)
 
 struct PartRes {
@@ -2251,6 +2260,13 @@ struct PWalk {
     uint64_t* seg_base;   // per segment: first record slot (B)
     uint2* recs;          // per part: kPartRec records of A's walk {offset, length << 8 | header}
     uint32_t pshift;      // log2 part bytes of this launch
+    // A's records past the first kPartRec of a part: blocks of kPartRec from a
+    // pool (one atomic per block), up to kMaxBlocks per part
+    uint2* pool;
+    uint32_t* pool_owner;            // per pool block: part * 16 + block number (1 ..)
+    uint32_t* blocks;                // per part: kMaxBlocks pool block indices
+    unsigned long long* pool_used;   // blocks taken (zeroed per launch)
+    uint64_t pool_cap;               // pool blocks
 };
 
 typedef const __attribute__((address_space(1))) uint32_t gu32;
@@ -2605,12 +2621,38 @@ __global__ __launch_bounds__(256) void k_walk_parts(PWalk w)
     __shared__ uint32_t tab[4 * 256];
     __shared__ uint2 lrec[256][kPartRec];
     walk_tab_fill(tab);
-    const int lane = threadIdx.x & (kWaveSize - 1);
     const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     const bool valid = i < w.nseg * w.nparts;
     PartRes r{};
     uint2* mine = lrec[threadIdx.x];
-    bool spill = false;
+    bool huge = false, lost = false;
+    // a full block of this lane's records to its place: block 0 to the
+    // part's scratch, later ones to pool blocks (a lane's 512 contiguous
+    // bytes; the lines fill up in L2)
+    auto put_block = [&](uint32_t b, uint32_t n) {
+        uint2* dst = nullptr;
+        if (b == 0) {
+            dst = w.recs + i * kPartRec;
+        } else if (b <= kMaxBlocks && !lost) {
+            const unsigned long long k = atomicAdd(w.pool_used, 1ull);
+            if (k < w.pool_cap) {
+                dst = w.pool + k * kPartRec;
+                w.blocks[i * kMaxBlocks + (b - 1)] = uint32_t(k);
+                w.pool_owner[k] = uint32_t(i * 16 + b);
+            }
+        }
+        if (!dst) {
+            lost = true;   // C walks the part again
+            return;
+        }
+        for (uint32_t e = 0; e < n; e += 2) {
+            const uint2 a0 = mine[e], a1 = mine[e + 1];
+            if (e + 1 < n)
+                *reinterpret_cast<uint4*>(dst + e) = make_uint4(a0.x, a0.y, a1.x, a1.y);
+            else
+                dst[e] = a0;
+        }
+    };
     if (valid) {
         const uint64_t seg = i / w.nparts;
         const uint32_t k = uint32_t(i - seg * w.nparts);
@@ -2629,26 +2671,34 @@ __global__ __launch_bounds__(256) void k_walk_parts(PWalk w)
             const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
             walk_lane(w, tab, seg, sb, start, pend < limit ? pend : limit, r,
                       [&](uint32_t idx, uint32_t pos, uint32_t len, uint32_t hdr) {
-                          if (idx < kPartRec)
-                              mine[idx] = make_uint2(pos, (len << 8) | hdr);
-                          spill = spill || len >= (1u << 24);
+                          // a part of at most kPartRec records keeps them in LDS
+                          // for the wave's coalesced flush below; a denser part
+                          // writes every full block as it goes
+                          if (idx == kPartRec)
+                              put_block(0, kPartRec);
+                          mine[idx & (kPartRec - 1)] = make_uint2(pos, (len << 8) | hdr);
+                          huge = huge || len >= (1u << 24);
+                          if (idx >= kPartRec && (idx & (kPartRec - 1)) == kPartRec - 1)
+                              put_block(idx / kPartRec, kPartRec);
                       },
                       1u << w.pshift);
-            if (r.count > kPartRec || spill)
+            if (r.count > kPartRec && (r.count & (kPartRec - 1)))
+                put_block(r.count / kPartRec, r.count & (kPartRec - 1));
+            if (r.count > kPartRec * (1 + kMaxBlocks) || huge || lost)
                 r.flags |= kPartSpill;
-            if (spill)
+            if (huge)
                 r.flags |= kPartHuge;
         }
         w.parts[i] = r;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS records
-    const bool flush = valid && (r.flags & kPartWalked) && !(r.flags & kPartHuge);
+    const int lane = threadIdx.x & (kWaveSize - 1);
+    const bool flush = valid && (r.flags & kPartWalked) && !(r.flags & kPartHuge) && r.count <= kPartRec;
     uint64_t todo = __ballot(flush);
     while (todo) {
         const int j = __builtin_ctzll(todo);
         todo &= todo - 1;
-        uint32_t n = __shfl(r.count, j, kWaveSize);
-        n = n < kPartRec ? n : kPartRec;
+        const uint32_t n = __shfl(r.count, j, kWaveSize);
         const uint64_t dst = (i - uint64_t(lane) + uint64_t(j)) * kPartRec;
         const uint2* src = lrec[(threadIdx.x & ~63u) + uint32_t(j)];
         for (uint32_t e = uint32_t(lane); e < n; e += kWaveSize)
@@ -3140,24 +3190,40 @@ __global__ __launch_bounds__(256) void k_walk_emit(PWalk w)
 // thread per record slot (consecutive threads copy consecutive records).
 __global__ __launch_bounds__(256) void k_walk_copy(PWalk w)
 {
+    // threads [0, parts * kPartRec): the parts' first blocks; then one per
+    // pool slot: the record it holds
     const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    const uint64_t i = t / kPartRec;
-    const uint32_t e = uint32_t(t - i * kPartRec);
-    if (i >= w.nseg * w.nparts)
-        return;
+    const uint64_t nfirst = w.nseg * w.nparts * kPartRec;
+    uint64_t i;
+    uint32_t ri;
+    uint2 v;
+    if (t < nfirst) {
+        i = t / kPartRec;
+        ri = uint32_t(t - i * kPartRec);
+        v = make_uint2(0u, 0u);
+    } else {
+        const uint64_t p = t - nfirst, blk = p / kPartRec;
+        if (blk >= *w.pool_used || blk >= w.pool_cap)
+            return;
+        const uint32_t own = w.pool_owner[blk];
+        i = own / 16;
+        ri = (own % 16) * kPartRec + uint32_t(p - blk * kPartRec);
+        v = w.pool[p];
+    }
     const PartRes& r = w.parts[i];
     const uint32_t fl = r.flags;
     if (!(fl & kPartEmit) || (fl & (kPartChase | kPartSpill)))
         return;
-    const uint32_t n = r.count - r.pre;
-    if (e >= n)
+    const uint32_t n = r.count - r.pre;   // records ri = cut .. cut + n - 1
+    if (ri < r.cut || ri - r.cut >= n)
         return;
     const uint64_t seg = i / w.nparts;
     if (w.fallback[seg])
         return;
-    const uint64_t dst = w.seg_base[seg] + r.rec + r.pre + e;
+    const uint64_t dst = w.seg_base[seg] + r.rec + r.pre + (ri - r.cut);
     if (dst < w.cap) {
-        const uint2 v = w.recs[i * kPartRec + r.cut + e];
+        if (t < nfirst)
+            v = w.recs[t];
         w.entries[dst] = u32x4{uint32_t(seg), v.x, v.y >> 8, v.y & 0xFF};
     }
 }
@@ -3394,6 +3460,10 @@ int ramcrc_ctx_destroy(ramcrc_ctx* c)
     if (c->walk_fallback) (void)hipFree(c->walk_fallback);
     if (c->walk_base) (void)hipFree(c->walk_base);
     if (c->walk_recs) (void)hipFree(c->walk_recs);
+    if (c->walk_pool) (void)hipFree(c->walk_pool);
+    if (c->walk_pool_owner) (void)hipFree(c->walk_pool_owner);
+    if (c->walk_blocks) (void)hipFree(c->walk_blocks);
+    if (c->walk_pool_used) (void)hipFree(c->walk_pool_used);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -3833,6 +3903,23 @@ int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_s
                              sizeof(uint64_t));
         if (!rc)
             rc = grow_device(&c->walk_recs, &c->walk_recs_cap, total * kPartRec, sizeof(uint2));
+        // the pool holds A's records past each part's first block: sized for
+        // entries of 96 B on average (denser parts than that, and records past
+        // entries_cap, fall back to C's second walk of the part)
+        uint64_t pool_blocks = (n_seg * uint64_t(seg_capacity) / 96) / kPartRec + 1;
+        const uint64_t cap_blocks = entries_cap / kPartRec + 1;
+        pool_blocks = pool_blocks < cap_blocks ? pool_blocks : cap_blocks;
+        if (!rc)
+            rc = grow_device(&c->walk_pool, &c->walk_pool_cap, pool_blocks * kPartRec, sizeof(uint2));
+        if (!rc)
+            rc = grow_device(reinterpret_cast<void**>(&c->walk_pool_owner), &c->walk_pool_owner_cap,
+                             pool_blocks, sizeof(uint32_t));
+        if (!rc)
+            rc = grow_device(reinterpret_cast<void**>(&c->walk_blocks), &c->walk_blocks_cap,
+                             total * kMaxBlocks, sizeof(uint32_t));
+        if (!rc)
+            rc = grow_device(reinterpret_cast<void**>(&c->walk_pool_used), &c->walk_pool_used_cap, 1,
+                             sizeof(unsigned long long));
         if (rc)
             return rc;
         PWalk pw{};
@@ -3851,6 +3938,12 @@ int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_s
         pw.seg_base = c->walk_base;
         pw.recs = static_cast<uint2*>(c->walk_recs);
         pw.pshift = pshift;
+        pw.pool = static_cast<uint2*>(c->walk_pool);
+        pw.pool_owner = c->walk_pool_owner;
+        pw.blocks = c->walk_blocks;
+        pw.pool_used = c->walk_pool_used;
+        pw.pool_cap = pool_blocks;
+        HIPCHK(hipMemsetAsync(c->walk_pool_used, 0, sizeof(unsigned long long), s));
         if (nparts > 1) {
             uint64_t g0 = (total + kSyncWaves - 1) / kSyncWaves;
             if (g0 > uint64_t(8) * c->ncu)
@@ -3864,7 +3957,8 @@ int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_s
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_walk_emit, dim3((total + 255) / 256), dim3(256), 0, s, pw);
         HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_walk_copy, dim3((total * kPartRec + 255) / 256), dim3(256), 0, s, pw);
+        hipLaunchKernelGGL(k_walk_copy, dim3(((total + pool_blocks) * kPartRec + 255) / 256), dim3(256),
+                           0, s, pw);
         HIPCHK(hipGetLastError());
         w.only = c->walk_fallback;
     }
