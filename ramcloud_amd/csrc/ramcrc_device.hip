@@ -2857,53 +2857,16 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
                         g = w.recs[pidx * kPartRec + uint32_t(lane)];
                     uint32_t p = pe, wc = 0, wnn = 0, wrr = 0, wflags = kPartWalked;
                     int cut = -1;
-                    uint2 mine = make_uint2(0u, 0u);   // record wc of the walk, in lane wc
-                    uint64_t mq = 0;                   // its header + length bytes
-                    bool huge = false;
-                    while (true) {
-                        const uint64_t hit = __ballot(uint32_t(lane) < gn && g.x == p);
-                        if (hit || (!(fl & kPartWrap) && p == st)) {
-                            cut = hit ? int(__builtin_ctzll(hit)) : 0;
-                            break;
-                        }
-                        if (p >= stop)
-                            break;
-                        if (wc >= budget) {
-                            wflags |= kPartWrap;   // out of budget: the serial walker
-                            break;
-                        }
-                        const uint64_t q = wpeek(p);
-                        const Hop h = hop_of(q, p);
-                        if (uint32_t(lane) == wc)
-                            mq = q;
-                        if (wc >= kWaveSize) {   // the first 64 are summed after the walk
-                            wrr = meta_update(tab, wrr, q, h.mbytes);
-                            wnn += h.mbytes;
-                        }
-                        if (h.next > 0xFFFFFFFFull) {
-                            wflags |= kPartWrap;
-                            break;
-                        }
-                        if (h.next > w.capacity) {
-                            wflags |= kPartOverrun;
-                            break;
-                        }
-                        if (uint32_t(lane) == wc)
-                            mine = make_uint2(p, (h.len << 8) | (uint32_t(q) & 0xFF));
-                        huge = huge || h.len >= (1u << 24);
-                        wc++;
-                        p = uint32_t(h.next);
-                    }
-                    rewalk += wc + 1;
-                    {
-                        // the header + length bytes of the walk's first 64 entries
-                        // (an entry that overran or wrapped included: the reference
-                        // checksums its header too), off the chase: each lane the
-                        // raw CRC of its entry's bytes moved past the later ones'
-                        // (suffix sums), XORed over the wave; then the entries after
-                        // the 64th, summed on the way
-                        const uint32_t seen = wc + ((wflags & (kPartWrap | kPartOverrun)) ? 1u : 0u);
-                        const bool inr = uint32_t(lane) < (seen < kWaveSize ? seen : uint32_t(kWaveSize));
+                    // the walk's records and header + length bytes, 64 at a time:
+                    // record wc in lane wc % 64; each full block's metadata CRC is
+                    // summed in parallel off the chase, and blocks 1.. go to pool
+                    // blocks (unattached until the walk proves to be a re-walk)
+                    uint2 mine = make_uint2(0u, 0u), mine0 = make_uint2(0u, 0u);
+                    uint64_t mq = 0;
+                    uint32_t myblk = 0xFFFFFFFFu;   // lane b: pool block of block b
+                    bool huge = false, pool_ok = true;
+                    auto fold_block = [&](uint32_t n) {   // lanes < n hold metadata
+                        const bool inr = uint32_t(lane) < n;
                         const uint32_t mb = inr ? uint32_t((mq >> 6) & 3) + 2 : 0u;
                         const uint32_t re = inr ? meta_update(tab, 0u, mq, mb) : 0u;
                         uint32_t incl = mb;
@@ -2918,8 +2881,77 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
 #pragma unroll
                         for (int s2 = 1; s2 < kWaveSize; s2 <<= 1)
                             hr ^= __shfl_xor(hr, s2, kWaveSize);
-                        wrr = mulmod_horner(hr, xpow8_dev(wnn)) ^ wrr;
+                        // raw(0, A||B) = X^|B|(raw(0, A)) ^ raw(0, B)
+                        wrr = mulmod_horner(wrr, xpow8_dev(hn)) ^ hr;
                         wnn += hn;
+                    };
+                    auto store_block = [&](uint32_t b, uint32_t n) {   // lanes < n hold records
+                        if (b == 0) {
+                            mine0 = mine;
+                            return;
+                        }
+                        if (!pool_ok || b > kMaxBlocks) {
+                            pool_ok = false;
+                            return;
+                        }
+                        unsigned long long k = 0;
+                        if (lane == 0)
+                            k = atomicAdd(w.pool_used, 1ull);
+                        k = __shfl(k, 0, kWaveSize);
+                        if (k >= w.pool_cap) {
+                            pool_ok = false;
+                            return;
+                        }
+                        if (uint32_t(lane) < n)
+                            w.pool[k * kPartRec + uint32_t(lane)] = mine;
+                        if (lane == 0)
+                            w.pool_owner[k] = 0xFFFFFFFFu;   // unattached
+                        if (uint32_t(lane) == b)
+                            myblk = uint32_t(k);
+                    };
+                    while (true) {
+                        const uint64_t hit = __ballot(uint32_t(lane) < gn && g.x == p);
+                        if (hit || (!(fl & kPartWrap) && p == st)) {
+                            cut = hit ? int(__builtin_ctzll(hit)) : 0;
+                            break;
+                        }
+                        if (p >= stop)
+                            break;
+                        if (wc >= budget) {
+                            wflags |= kPartWrap;   // out of budget: the serial walker
+                            break;
+                        }
+                        const uint64_t q = wpeek(p);
+                        const Hop h = hop_of(q, p);
+                        if (uint32_t(lane) == (wc & (kWaveSize - 1)))
+                            mq = q;
+                        if (h.next > 0xFFFFFFFFull) {
+                            wflags |= kPartWrap;
+                            break;
+                        }
+                        if (h.next > w.capacity) {
+                            wflags |= kPartOverrun;
+                            break;
+                        }
+                        if (uint32_t(lane) == (wc & (kWaveSize - 1)))
+                            mine = make_uint2(p, (h.len << 8) | (uint32_t(q) & 0xFF));
+                        huge = huge || h.len >= (1u << 24);
+                        wc++;
+                        p = uint32_t(h.next);
+                        if ((wc & (kWaveSize - 1)) == 0) {
+                            fold_block(kWaveSize);
+                            store_block(wc / kWaveSize - 1, kWaveSize);
+                        }
+                    }
+                    rewalk += wc + 1;
+                    {
+                        // the last partial block's header + length bytes (with an
+                        // entry that overran or wrapped: the reference checksums its
+                        // header too)
+                        const uint32_t rem = (wc & (kWaveSize - 1)) +
+                                             ((wflags & (kPartWrap | kPartOverrun)) ? 1u : 0u);
+                        if (rem)
+                            fold_block(rem);
                     }
                     if (cut >= 0 && (fl & kPartWrap)) {
                         wflags |= kPartWrap;   // met a chain that wraps: the serial walker
@@ -2967,12 +2999,30 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
 #ifdef RAMCRC_WALK_DEBUG
                         dbg_chase++;
 #endif
-                        // walked the whole part: its records go to the scratch
-                        // (C copies them), or, more than it holds, C walks it again
+                        // walked the whole part: its records go to the scratch and
+                        // pool blocks (C copies them), or, when they do not fit, C
+                        // walks it again
                         jex = p;
-                        const bool keep = wc <= kPartRec && !huge;
-                        if (keep && uint32_t(lane) < wc)
-                            w.recs[pidx * kPartRec + uint32_t(lane)] = mine;
+                        if (wc > kPartRec && (wc & (kPartRec - 1)))
+                            store_block(wc / kPartRec, wc & (kPartRec - 1));
+                        const bool keep = !huge && pool_ok && wc <= kPartRec * (1 + kMaxBlocks);
+                        if (keep) {
+                            const uint2 first = wc <= kPartRec ? mine : mine0;
+                            if (uint32_t(lane) < (wc < kPartRec ? wc : kPartRec))
+                                w.recs[pidx * kPartRec + uint32_t(lane)] = first;
+                            // replace A's blocks of this part by the walk's
+                            const uint32_t nb = (wc + kPartRec - 1) / kPartRec;   // blocks incl. 0
+                            if (lane >= 1 && uint32_t(lane) <= kMaxBlocks) {
+                                const uint32_t own = uint32_t(pidx * 16 + uint32_t(lane));
+                                const uint32_t old = w.blocks[pidx * kMaxBlocks + uint32_t(lane) - 1];
+                                if (old < w.pool_cap && w.pool_owner[old] == own)
+                                    w.pool_owner[old] = 0xFFFFFFFFu;
+                                if (uint32_t(lane) < nb) {
+                                    w.blocks[pidx * kMaxBlocks + uint32_t(lane) - 1] = myblk;
+                                    w.pool_owner[myblk] = own;
+                                }
+                            }
+                        }
                         if (lane == j) {
                             r.start = pe;
                             r.exit = p;
@@ -3206,6 +3256,8 @@ __global__ __launch_bounds__(256) void k_walk_copy(PWalk w)
         if (blk >= *w.pool_used || blk >= w.pool_cap)
             return;
         const uint32_t own = w.pool_owner[blk];
+        if (own == 0xFFFFFFFFu)
+            return;   // a block the fix-up wrote for a walk that met the guess
         i = own / 16;
         ri = (own % 16) * kPartRec + uint32_t(p - blk * kPartRec);
         v = w.pool[p];
