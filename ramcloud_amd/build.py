@@ -91,6 +91,10 @@ VARIANTS = {
     "ps15": ["RAMCRC_PART_SHIFT=15"],
     "ps17": ["RAMCRC_PART_SHIFT=17"],
     "tv1": ["RAMCRC_TINY_V=1"],
+    "notrim": ["RAMCRC_TINY_TRIM=0"],
+    "tinyprobe": ["RAMCRC_TINY_PROBE=1", "RAMCRC_TINY_CF=0"],
+    "nocf": ["RAMCRC_TINY_CF=0"],
+    "aa": ["RAMCRC_AA_SAME=1"],   # A/A: identical code, separate library
     # k_entries ping-pong depth / waves per CU
     "pu4": ["RAMCRC_PU=4"],
     "ew8": ["RAMCRC_ENT_WAVES=8"],

@@ -89,6 +89,9 @@ struct alignas(16) DeviceTables {
     uint32_t xblk[4][256];  // x^(8 * 1024 * b * 256^j)
     uint32_t xinv[1024];    // x^(-8 p)
     uint32_t pos[132][256]; // k_entries, tiny phase: row r = X^(r-3)(byte), rows 0..3 (m <= 0) zero
+    // The same rows laid out for conflict-free lookups (tiny phase, RAMCRC_TINY_CF):
+    // word 128 (255 - b) + (128 - m) = X^m(b), m = 1 .. 128, then 128 zero words.
+    uint32_t post[256 * 128 + 128];
     uint32_t xmeta[5 * 64 + 1];   // k_seg_walk: x^(8d), d = 0 .. 320 (one batch of metadata)
     uint32_t xbyte[4][256];       // x^(8 * b * 256^j): x^(8d) for any 32-bit d in 4 factors
 };
@@ -118,8 +121,10 @@ constexpr DeviceTables make_device_tables()
     }
     for (int m = 1; m <= 128; m++) {
         const uint32_t c = ramcrc::xpow8(uint64_t(m));
-        for (uint32_t b = 0; b < 256; b++)
+        for (uint32_t b = 0; b < 256; b++) {
             t.pos[m + 3][b] = ramcrc::mulmod(b, c);
+            t.post[128 * (255 - b) + (128 - m)] = t.pos[m + 3][b];
+        }
     }
     for (int d = 0; d <= 5 * 64; d++)
         t.xmeta[d] = ramcrc::xpow8(uint64_t(d));
@@ -752,6 +757,15 @@ constexpr int kSmallK = RAMCRC_SMALLK;     // bins 2..kSmallK: octets loaded one
 #define RAMCRC_PU 2   // A/B on the config-3 mix, 1 KiB and 4 KiB entries: 2 < 1, 3, 4, 6, 8
 #endif
 constexpr int kPU = RAMCRC_PU;             // ping-pong depth (pipelined bins)
+#ifndef RAMCRC_TINY_TRIM
+#define RAMCRC_TINY_TRIM 1   // tiny phase: 64-bit-shift head masks, saturating row bases
+#endif
+#ifndef RAMCRC_TINY_CF
+#define RAMCRC_TINY_CF 1     // tiny phase: conflict-free column-major table (tiny_run_cf)
+#endif
+#ifndef RAMCRC_TINY_PROBE
+#define RAMCRC_TINY_PROBE 0  // A/B only: conflict-free lookup addresses, wrong CRCs
+#endif
 constexpr uint32_t kNoIdx = 0xFFFFFFFFu;   // empty slot
 constexpr uint64_t kOctetCost = 4;         // per-octet overhead in step units (work split)
 constexpr int kBinPer = 4;                 // entries per thread per tile (count/scatter)
@@ -1199,6 +1213,34 @@ __device__ __forceinline__ void tiny_run(const BatchDesc& d, const Sorted& so, u
             const int e = sa + int(len) - 16 * gl;       // E - a (<= 128)
             const uint32_t ws[4] = {wc[q].x, wc[q].y, wc[q].z, wc[q].w};
             uint32_t v[16];
+#if RAMCRC_TINY_TRIM
+            // Only lane 0 of the group holds bytes before S (ds = S - a is
+            // 0..15 there and negative elsewhere): h8 = bits to drop from the
+            // bottom of the lane's 128 bits.  Dword j drops clamp(h8 - 32 j,
+            // 0, 32) bits: one 64-bit shift makes the mask, 0 at 32.  The row
+            // base max(e - 4 j, 0) * 256 is one saturating subtract from
+            // max(e, 0) * 256.
+            const int h8 = max(ds, 0) * 8;
+            const uint32_t eb = uint32_t(max(e, 0)) << 10;   // bytes
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t drop = uint32_t(min(max(h8 - 32 * j, 0), 32));
+                const uint32_t x = ws[j] & uint32_t(~uint64_t(0) << drop);
+                const uint32_t base = __builtin_elementwise_sub_sat(eb, uint32_t(4096 * j));
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+#if RAMCRC_TINY_PROBE
+                    // bank-conflict probe (WRONG results): bank = lane & 31
+                    const uint32_t ad = ((base | (((x >> (8 * t)) & 0xFF) << 2)) & ~0x7Cu) |
+                                        ((uint32_t(lane) & 31) << 2);
+#else
+                    const uint32_t ad = base | (((x >> (8 * t)) & 0xFF) << 2);
+#endif
+                    v[4 * j + t] = *reinterpret_cast<const uint32_t*>(
+                        lds + ad + (kTinyRow0 - t) * 1024);
+                }
+            }
+#else
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const uint32_t x = ws[j] & ~keep_lo(ds - 4 * j);
@@ -1207,6 +1249,7 @@ __device__ __forceinline__ void tiny_run(const BatchDesc& d, const Sorted& so, u
                 for (int t = 0; t < 4; t++)
                     v[4 * j + t] = tab[base + ((x >> (8 * t)) & 0xFF) + (kTinyRow0 - t) * 256];
             }
+#endif
             const uint32_t t0 = xor3(v[0], v[1], v[2]), t1 = xor3(v[3], v[4], v[5]);
             const uint32_t t2 = xor3(v[6], v[7], v[8]), t3 = xor3(v[9], v[10], v[11]);
             const uint32_t t4 = xor3(v[12], v[13], v[14]);
@@ -1229,6 +1272,168 @@ __device__ __forceinline__ void tiny_run(const BatchDesc& d, const Sorted& so, u
                 R = o0.init;
                 for (uint32_t k = 0; k < o0.len; k++)
                     R = tab[(1 + kTinyRow0) * 256 + ((R ^ *(const gu8*)(o0.S + k)) & 0xFF)] ^ (R >> 8);
+            }
+            const uint32_t Rf = finalize ? ~R : R;
+            d.out[o0.ix] = Rf;
+            if (d.vstat && Rf != sc)
+                atomicAdd(&d.vstat[d.rec[o0.ix].x].bad_objects, 1u);
+        }
+        o0 = o1;
+        o1 = o2;
+        sc = sn;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            wc[q] = wn[q];
+            gc[q] = gn[q];
+        }
+    }
+}
+
+// The tiny phase with conflict-free table lookups (RAMCRC_TINY_CF).  The
+// position table is laid out column-major, byte address 512 (255 - b) +
+// 4 (128 - m) for X^m(b) (g_tab.post), so a lookup's LDS bank is (128 - m)
+// mod 32 whatever the data byte.  Lane u of a group holds the window dwords
+// u, u + 8, u + 16, u + 24 (window offsets 32 j + 4 u), so the 8 lanes of a
+// group read 8 rows 4 apart: 8 banks of one residue class mod 4.  Each group
+// takes the bytes of its dwords in a rotated order, byte (k + c) & 3 at
+// instruction k with c = (e + g) & 3 (e the window-relative entry end, g the
+// group's index in its 32-lane half), which puts the 4 groups of a half on the
+// 4 residue classes: the 32 lanes of a ds_read_b32 group hit 32 banks.  Bytes
+// outside the entry are masked to 0 and complemented to column 255, whose
+// rows, and the 128 words after the table, are zero; so no zero rows and
+// no clamps are needed.  Round structure, descriptor ownership and the init
+// fold are those of tiny_run.
+__device__ __forceinline__ void tiny_run_cf(const BatchDesc& d, const Sorted& so, uint8_t* lds)
+{
+    if (so.bt->start[2] == so.bt->start[0])
+        return;   // no entry of at most one window (uniform: every wave exits)
+    const int lane = threadIdx.x & (kWaveSize - 1);
+    const uint32_t gl = uint32_t(lane) & 7;
+    const uint32_t g4 = (uint32_t(lane) >> 3) & 3;
+    const uint64_t wave = uint64_t(blockIdx.x) * kEntWaves +
+                          __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
+    const uint64_t nwaves = uint64_t(gridDim.x) * kEntWaves;
+    const uint64_t s0 = so.bt->start[0], s1 = so.bt->start[2];
+    const uint64_t rounds = (s1 - s0 + 63) / 64;
+    const bool finalize = d.flags & RAMCRC_FINALIZE;
+    const uint64_t dummy = reinterpret_cast<uint64_t>(so.bt);
+    typedef const __attribute__((address_space(1))) uint32_t g32;
+
+    auto load_own = [&](uint64_t r) -> TinyOwn {
+        TinyOwn o;
+        const uint64_t sl = s0 + r * 64 + uint32_t(lane);
+        u32x4 dd = {0u, 0u, 0u, 0u};
+        o.ix = kNoIdx;
+        o.init = 0xFFFFFFFFu;
+        if (r < rounds && sl < s1) {
+            dd = so.desc[sl];
+            o.ix = so.idx[sl];
+            if (d.init)
+                o.init = so.init[sl];
+        }
+        o.S = (uint64_t(dd.y) << 32) | dd.x;
+        const uint64_t E = (uint64_t(dd.w) << 32) | dd.z;
+        o.len = uint32_t(E - o.S);
+        o.A = o.S & ~uint64_t(15);
+        o.geo = (o.ix != kNoIdx && o.len >= 4) ? (o.len | (uint32_t(o.S - o.A) << 8)) : 0u;
+        if (!o.geo)
+            o.A = dummy;   // nothing to hash: the window loads read valid memory
+        return o;
+    };
+    // the group's eight windows: dwords gl + 8 j of each owner's window.  A
+    // dword that starts at or past E loads the entry's last dword instead
+    // (its bytes are masked), so no load leaves the entry's last dword.
+    auto issue = [&](const TinyOwn& o, u32x4 (&w)[8], uint32_t (&geo)[8], uint32_t& st) {
+        st = d.vstat && o.ix != kNoIdx ? load_u32_any(o.S - 4) : 0u;
+        static_for8([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            geo[q] = swz_from<q>(o.geo);
+            const uint64_t A = (uint64_t(swz_from<q>(uint32_t(o.A >> 32))) << 32) |
+                               swz_from<q>(uint32_t(o.A));
+            const uint32_t e = ((geo[q] >> 8) & 0xF) + (geo[q] & 0xFF);   // E - A (0: empty)
+            const int el = (max(int(e) - 1, 0) & ~3) - int(4 * gl);   // last dword, from 4 u
+            const uint64_t au = A + 4 * gl;
+            u32x4 v;
+            v.x = *reinterpret_cast<g32*>(au + min(0, el));
+            v.y = *reinterpret_cast<g32*>(au + min(32, el));
+            v.z = *reinterpret_cast<g32*>(au + min(64, el));
+            v.w = *reinterpret_cast<g32*>(au + min(96, el));
+            w[q] = v;
+        });
+    };
+    // X^m(b) in the column-major table
+    auto tabv = [&](uint32_t m, uint32_t b) -> uint32_t {
+        return *reinterpret_cast<const uint32_t*>(lds + 512 * (255 - b) + 4 * (128 - m));
+    };
+
+    uint64_t r = wave;
+    TinyOwn o0 = load_own(r), o1 = load_own(r + nwaves);
+    fill_plain(lds, 0, g_tab.post, 256 * 128 + 128);
+    __syncthreads();
+    u32x4 wc[8];
+    uint32_t gc[8], sc;
+    issue(o0, wc, gc, sc);
+    for (; r < rounds; r += nwaves) {
+        const TinyOwn o2 = load_own(r + 2 * nwaves);
+        u32x4 wn[8];
+        uint32_t gn[8], sn = 0;
+        if (r + nwaves < rounds)
+            issue(o1, wn, gn, sn);
+        uint32_t mine = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const uint32_t sa = (gc[q] >> 8) & 0xF;
+            const uint32_t e = sa + (gc[q] & 0xFF);           // window-relative end, <= 128
+            const uint32_t c = (e + g4) & 3;                  // byte rotation of this group
+            const uint32_t bb = 512 - 4 * e + 16 * gl;        // 4 (128 - e + 4 u): row of offset 4 u
+            const uint32_t rot = __builtin_amdgcn_alignbyte(0x0C080400u, 0x0C080400u, c);
+            // byte k of the rotated dword sits at window offset 4 u + ((k + c) & 3)
+            // (row bits below 512 for every byte of the entry; a masked byte's
+            // column 255 is zero at every row, so OR-ing its larger row is safe)
+            uint32_t pk[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                pk[k] = bb + ((rot >> (8 * k)) & 0xFF);
+            // tail: dword j keeps its bytes before E, clamp(e - 32 j - 4 u, 0, 4)
+            const int z = 32 - 8 * int(e) + 32 * int(gl);   // bits to drop from dword 0's top
+            // head: window bytes before S lie in dword 0 of lanes 0-3
+            const uint32_t hd = uint32_t(min(max(8 * (int(sa) - 4 * int(gl)), 0), 32));
+            const uint32_t ws[4] = {wc[q].x, wc[q].y, wc[q].z, wc[q].w};
+            uint32_t v[16];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t sh = uint32_t(min(max(z + 256 * j, 0), 32));
+                uint32_t keep = uint32_t(uint64_t(0xFFFFFFFFu) >> sh);
+                if (j == 0)
+                    keep &= uint32_t(~uint64_t(0) << hd);
+                const uint32_t xb = ~(ws[j] & keep);          // masked bytes -> column 255
+                const uint32_t xr = __builtin_amdgcn_alignbyte(xb, xb, c);
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    v[4 * j + k] = *reinterpret_cast<const uint32_t*>(
+                        lds + ((((xr >> (8 * k)) & 0xFF) << 9) | pk[k]) + 128 * j);
+            }
+            const uint32_t t0 = xor3(v[0], v[1], v[2]), t1 = xor3(v[3], v[4], v[5]);
+            const uint32_t t2 = xor3(v[6], v[7], v[8]), t3 = xor3(v[9], v[10], v[11]);
+            const uint32_t t4 = xor3(v[12], v[13], v[14]);
+            uint32_t R = xor3(xor3(t0, t1, t2), xor3(t3, t4, v[15]), 0u);
+            R ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(R), 0xB1, 0xF, 0xF, false));   // lane ^ 1
+            R ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(R), 0x4E, 0xF, 0xF, false));   // lane ^ 2
+            R ^= uint32_t(__builtin_amdgcn_ds_swizzle(int(R), 0x1F | (4 << 10)));           // lane ^ 4
+            mine = gl == uint32_t(q) ? R : mine;
+        }
+        // own slot: the initial state (byte k at distance len - k), or bytewise
+        if (o0.ix != kNoIdx) {
+            uint32_t R;
+            if (o0.len >= 4) {
+                const uint32_t in = o0.init, n = o0.len;
+                R = mine ^ xor3(tabv(n, in & 0xFF), tabv(n - 1, (in >> 8) & 0xFF),
+                                tabv(n - 2, (in >> 16) & 0xFF)) ^
+                    tabv(n - 3, in >> 24);
+            } else {
+                R = o0.init;
+                for (uint32_t k = 0; k < o0.len; k++)
+                    R = tabv(1, (R ^ *(const gu8*)(o0.S + k)) & 0xFF) ^ (R >> 8);
             }
             const uint32_t Rf = finalize ? ~R : R;
             d.out[o0.ix] = Rf;
@@ -1566,7 +1771,11 @@ __global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc 
             so.bt->cursor[t] = 0;
         }
     }
+#if RAMCRC_TINY_CF
+    tiny_run_cf(d, so, lds);
+#else
     tiny_run(d, so, lds);
+#endif
     if (so.bt->items[2] == so.bt->items[kNB])
         return;   // every entry is tiny (or large on the batch path)
     __syncthreads();   // the position table is dead: refill the LDS
