@@ -94,6 +94,8 @@ VARIANTS = {
     "notrim": ["RAMCRC_TINY_TRIM=0"],
     "tinyprobe": ["RAMCRC_TINY_PROBE=1", "RAMCRC_TINY_CF=0"],
     "nocf": ["RAMCRC_TINY_CF=0"],
+    "bg1": ["RAMCRC_BIN_WGS_PER_CU=1"],
+    "bg4": ["RAMCRC_BIN_WGS_PER_CU=4"],
     "aa": ["RAMCRC_AA_SAME=1"],   # A/A: identical code, separate library
     # k_entries ping-pong depth / waves per CU
     "pu4": ["RAMCRC_PU=4"],

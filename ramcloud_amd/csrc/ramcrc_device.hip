@@ -769,6 +769,10 @@ constexpr int kPU = RAMCRC_PU;             // ping-pong depth (pipelined bins)
 constexpr uint32_t kNoIdx = 0xFFFFFFFFu;   // empty slot
 constexpr uint64_t kOctetCost = 4;         // per-octet overhead in step units (work split)
 constexpr int kBinPer = 4;                 // entries per thread per tile (count/scatter)
+#ifndef RAMCRC_BIN_WGS_PER_CU
+#define RAMCRC_BIN_WGS_PER_CU 8
+#endif
+constexpr uint64_t kBinWgsPerCu = RAMCRC_BIN_WGS_PER_CU;   // binning grid cap per CU
 
 constexpr uint32_t kTinyRow0 = 3;            // tiny phase: row of distance m is m + 3
 constexpr uint32_t kLdsTiny = 132 * 1024;    // tiny phase: X^m(byte), m = -3..128
@@ -2081,9 +2085,12 @@ int launch_binned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_lar
     if (rc)
         return rc;
     Sorted so{c->bins, c->sdesc, c->sidx, c->sinit};
+    // One tile per workgroup up to kBinWgsPerCu workgroups per CU: the binning
+    // passes are latency-bound loads of 16 B per entry, and one 4-wave
+    // workgroup per CU walking its tiles in turn kept one tile in flight.
     uint64_t grid = (d.n + uint64_t(kThreads) * kBinPer - 1) / (uint64_t(kThreads) * kBinPer);
-    if (grid > uint64_t(c->ncu))
-        grid = c->ncu;
+    if (grid > uint64_t(c->ncu) * kBinWgsPerCu)
+        grid = uint64_t(c->ncu) * kBinWgsPerCu;
     hipLaunchKernelGGL(k_bin_count<kMode>, dim3(grid), dim3(kThreads), 0, s, d, so, skip_large);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_bin_scatter<kMode>, dim3(grid), dim3(kThreads), 0, s, d, so, skip_large);
