@@ -39,6 +39,7 @@
 //
 // No MFMA: this is a byte scan, bound by HBM reads.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <mutex>
 #include <new>
@@ -2027,6 +2028,13 @@ Plan make_plan(ramcrc_ctx* c, uint64_t n)
 // elapsed time is read only after the stream is synchronised.
 constexpr unsigned kTimerEventFlags = hipEventDisableSystemFence;
 
+#ifndef RAMCRC_EXT_TIMING
+#define RAMCRC_EXT_TIMING 1
+#endif
+// Times the one launch of its scope.  With RAMCRC_EXT_TIMING the two events
+// ride in the kernel's own dispatch (hipExtLaunchKernelGGL start/stop
+// events): no separate event packets, so no stream bubble before and after
+// the kernel; otherwise they are recorded around it.
 struct ScanTimer {
     ramcrc_ctx* c;
     hipStream_t s;
@@ -2043,13 +2051,23 @@ struct ScanTimer {
             ev = {nullptr, nullptr};
             return;
         }
-        (void)hipEventRecord(ev.first, s);
+        if (!RAMCRC_EXT_TIMING)
+            (void)hipEventRecord(ev.first, s);
+    }
+    template <typename F, typename... Args>
+    void launch(F kernel, dim3 grid, dim3 block, Args... args)
+    {
+        if (RAMCRC_EXT_TIMING && ev.first)
+            hipExtLaunchKernelGGL(kernel, grid, block, 0, s, ev.first, ev.second, 0, args...);
+        else
+            hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
     }
     ~ScanTimer()
     {
         if (!ev.first)
             return;
-        (void)hipEventRecord(ev.second, s);
+        if (!RAMCRC_EXT_TIMING)
+            (void)hipEventRecord(ev.second, s);
         c->ev_used.push_back(ev);
     }
 };
@@ -2097,7 +2115,7 @@ int launch_binned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_lar
     HIPCHK(hipGetLastError());
     {
         ScanTimer t(c, s);
-        hipLaunchKernelGGL(k_entries, dim3(c->ncu), dim3(kEntWaves * kWaveSize), 0, s, d, so);
+        t.launch(k_entries, dim3(c->ncu), dim3(kEntWaves * kWaveSize), d, so);
     }
     HIPCHK(hipGetLastError());
     return RAMCRC_OK;
@@ -2113,8 +2131,7 @@ int launch_planned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s)
     HIPCHK(hipGetLastError());
     {
         ScanTimer t(c, s);
-        hipLaunchKernelGGL(k_chunks<kMode>, dim3(c->ncu), dim3(kThreads), 0, s, d, pl,
-                           uint64_t(0));
+        t.launch(k_chunks<kMode>, dim3(c->ncu), dim3(kThreads), d, pl, uint64_t(0));
     }
     HIPCHK(hipGetLastError());
     if (d.n > kWideCombineMin)
@@ -3903,8 +3920,7 @@ int ramcrc_segments_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_bytes
         Plan pl = make_plan(c, 0);
         {
             ScanTimer t(c, s);
-            hipLaunchKernelGGL(k_chunks<kSegAligned>, dim3(c->ncu), dim3(kThreads), 0, s, d, pl,
-                               per);
+            t.launch(k_chunks<kSegAligned>, dim3(c->ncu), dim3(kThreads), d, pl, per);
         }
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL((k_combine<kSegAligned, false>), dim3((nseg + 3) / 4), dim3(256), 0, s,
