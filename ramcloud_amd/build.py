@@ -97,6 +97,8 @@ VARIANTS = {
     "bg1": ["RAMCRC_BIN_WGS_PER_CU=1"],
     "bg4": ["RAMCRC_BIN_WGS_PER_CU=4"],
     "evrec": ["RAMCRC_EXT_TIMING=0"],
+    "bp2": ["RAMCRC_BIN_PER=2"],
+    "bp8": ["RAMCRC_BIN_PER=8"],
     "aa": ["RAMCRC_AA_SAME=1"],   # A/A: identical code, separate library
     # k_entries ping-pong depth / waves per CU
     "pu4": ["RAMCRC_PU=4"],

@@ -769,7 +769,10 @@ constexpr int kPU = RAMCRC_PU;             // ping-pong depth (pipelined bins)
 #endif
 constexpr uint32_t kNoIdx = 0xFFFFFFFFu;   // empty slot
 constexpr uint64_t kOctetCost = 4;         // per-octet overhead in step units (work split)
-constexpr int kBinPer = 4;                 // entries per thread per tile (count/scatter)
+#ifndef RAMCRC_BIN_PER
+#define RAMCRC_BIN_PER 4
+#endif
+constexpr int kBinPer = RAMCRC_BIN_PER;    // entries per thread per tile (count/scatter)
 #ifndef RAMCRC_BIN_WGS_PER_CU
 #define RAMCRC_BIN_WGS_PER_CU 8
 #endif
