@@ -99,6 +99,7 @@ VARIANTS = {
     "evrec": ["RAMCRC_EXT_TIMING=0"],
     "bp2": ["RAMCRC_BIN_PER=2"],
     "bp8": ["RAMCRC_BIN_PER=8"],
+    "nosafe": ["RAMCRC_TINY_SAFE=0"],
     "aa": ["RAMCRC_AA_SAME=1"],   # A/A: identical code, separate library
     # k_entries ping-pong depth / waves per CU
     "pu4": ["RAMCRC_PU=4"],

@@ -764,6 +764,9 @@ constexpr int kPU = RAMCRC_PU;             // ping-pong depth (pipelined bins)
 #ifndef RAMCRC_TINY_CF
 #define RAMCRC_TINY_CF 1     // tiny phase: conflict-free column-major table (tiny_run_cf)
 #endif
+#ifndef RAMCRC_TINY_SAFE
+#define RAMCRC_TINY_SAFE 1    // tiny_run_cf: unclamped window loads when every window of a q is page-safe
+#endif
 #ifndef RAMCRC_TINY_PROBE
 #define RAMCRC_TINY_PROBE 0  // A/B only: conflict-free lookup addresses, wrong CRCs
 #endif
@@ -1346,11 +1349,18 @@ __device__ __forceinline__ void tiny_run_cf(const BatchDesc& d, const Sorted& so
         o.geo = (o.ix != kNoIdx && o.len >= 4) ? (o.len | (uint32_t(o.S - o.A) << 8)) : 0u;
         if (!o.geo)
             o.A = dummy;   // nothing to hash: the window loads read valid memory
+        // bit 12: the whole window [A, A + 128) lies in pages that hold entry
+        // bytes (or in the bin table), so its dwords can be read unclamped
+        const bool safe = !o.geo || ((o.A + 127) >> 12) == ((E - 1) >> 12);
+        o.geo |= safe ? (1u << 12) : 0u;
         return o;
     };
-    // the group's eight windows: dwords gl + 8 j of each owner's window.  A
-    // dword that starts at or past E loads the entry's last dword instead
-    // (its bytes are masked), so no load leaves the entry's last dword.
+    // the group's eight windows: dwords gl + 8 j of each owner's window.
+    // Bytes outside the entry are masked, so a dword past E may hold
+    // anything: when all eight windows of a q stay inside pages that hold
+    // entry bytes (bit 12 of geo), the dwords are read as they are; otherwise
+    // a dword that starts at or past E loads the entry's last dword instead,
+    // so no load leaves the entry's last dword.
     auto issue = [&](const TinyOwn& o, u32x4 (&w)[8], uint32_t (&geo)[8], uint32_t& st) {
         st = d.vstat && o.ix != kNoIdx ? load_u32_any(o.S - 4) : 0u;
         static_for8([&](auto qc) {
@@ -1358,14 +1368,22 @@ __device__ __forceinline__ void tiny_run_cf(const BatchDesc& d, const Sorted& so
             geo[q] = swz_from<q>(o.geo);
             const uint64_t A = (uint64_t(swz_from<q>(uint32_t(o.A >> 32))) << 32) |
                                swz_from<q>(uint32_t(o.A));
-            const uint32_t e = ((geo[q] >> 8) & 0xF) + (geo[q] & 0xFF);   // E - A (0: empty)
-            const int el = (max(int(e) - 1, 0) & ~3) - int(4 * gl);   // last dword, from 4 u
             const uint64_t au = A + 4 * gl;
             u32x4 v;
-            v.x = *reinterpret_cast<g32*>(au + min(0, el));
-            v.y = *reinterpret_cast<g32*>(au + min(32, el));
-            v.z = *reinterpret_cast<g32*>(au + min(64, el));
-            v.w = *reinterpret_cast<g32*>(au + min(96, el));
+            if (RAMCRC_TINY_SAFE && __builtin_amdgcn_ballot_w64(!((geo[q] >> 12) & 1)) == 0) {
+                // every window of this q is page-safe: plain loads, immediate offsets
+                v.x = *reinterpret_cast<g32*>(au);
+                v.y = *reinterpret_cast<g32*>(au + 32);
+                v.z = *reinterpret_cast<g32*>(au + 64);
+                v.w = *reinterpret_cast<g32*>(au + 96);
+            } else {
+                const uint32_t e = ((geo[q] >> 8) & 0xF) + (geo[q] & 0xFF);   // E - A (0: empty)
+                const int el = (max(int(e) - 1, 0) & ~3) - int(4 * gl);   // last dword, from 4 u
+                v.x = *reinterpret_cast<g32*>(au + min(0, el));
+                v.y = *reinterpret_cast<g32*>(au + min(32, el));
+                v.z = *reinterpret_cast<g32*>(au + min(64, el));
+                v.w = *reinterpret_cast<g32*>(au + min(96, el));
+            }
             w[q] = v;
         });
     };
