@@ -38,8 +38,11 @@ enum {
     RAMCRC_EHIP = -3,     /* a HIP runtime call failed; see ramcrc_last_hip_error */
     RAMCRC_ENODEV = -4,   /* no usable gfx950 device */
     RAMCRC_ERCCL = -5,    /* RCCL failure or RCCL unavailable (multi-GPU shard) */
-    RAMCRC_EREFUSED = -6  /* a launch found more chunks than the context's scratch holds and
+    RAMCRC_EREFUSED = -6, /* a launch found more chunks than the context's scratch holds and
                              wrote none of its outputs (see ramcrc_ctx_check) */
+    RAMCRC_EINTERNAL = -7 /* a small-entry launch found its bin layout inconsistent with the
+                             entries it binned and wrote none of its outputs (an internal
+                             invariant; never expected -- see ramcrc_ctx_check) */
 };
 
 /* Output flag: apply the final inversion (Crc32C::getResult, src/Crc32C.h:247).
@@ -360,6 +363,17 @@ int ramcrc_assemble_objects_host(ramcrc_ctx* ctx, void* const* objs, const uint6
  *                           parity tests run several); smaller parts measured
  *                           no faster even on segments of 100-byte entries. */
 #define RAMCRC_OPT_WALK_PART_SHIFT 2
+/*   RAMCRC_OPT_TEST_FAIL_AFTER_COUNT  test hook: the next `value` small-entry
+ *                           launch sequences return RAMCRC_EHIP right after
+ *                           their histogram pass is enqueued (the launch
+ *                           failure the error paths must survive); 0: off. */
+#define RAMCRC_OPT_TEST_FAIL_AFTER_COUNT 3
+/*   RAMCRC_OPT_TEST_DIRTY_BINS  test hook: the next small-entry launch adds
+ *                           (value & 0xffff) to the histogram count of bin
+ *                           value >> 16 between its count and scatter passes;
+ *                           the launch must then refuse (RAMCRC_EINTERNAL from
+ *                           ramcrc_ctx_check) rather than read stale slots. */
+#define RAMCRC_OPT_TEST_DIRTY_BINS 4
 int ramcrc_ctx_set_option(ramcrc_ctx* ctx, int option, int64_t value);
 
 /* Kernel timing (for benchmarks): when enabled, every launch brackets its
@@ -388,12 +402,15 @@ int ramcrc_ctx_set_cus(ramcrc_ctx* ctx, int ncu);
 
 /* Raw launch status word of the context (bit 0: the latest planned launch
  * found more chunks than the scratch holds and wrote none of its outputs;
- * bit 1: some launch did since the last ramcrc_ctx_check).  Synchronous. */
+ * bit 1: some launch refused since the last ramcrc_ctx_check; bit 2: one of
+ * them was a small-entry launch whose bin layout was inconsistent).
+ * Synchronous. */
 int ramcrc_ctx_status(ramcrc_ctx* ctx, uint32_t* status);
 
-/* Waits for `stream`, then returns RAMCRC_EREFUSED (and clears the sticky
- * bit) if any launch of this context was refused since the last check,
- * RAMCRC_OK otherwise.  A refusal needs a general batch whose buffers
+/* Waits for `stream`, then returns RAMCRC_EINTERNAL or RAMCRC_EREFUSED (and
+ * clears the sticky bits, atomically on the device) if any launch of this
+ * context was refused since the last check, RAMCRC_OK otherwise.  A refusal
+ * needs a general batch whose buffers
  * overlap or total more bytes than the device holds (ramcrc_batch_device,
  * ramcrc_verify_objects_device, ramcrc_assemble_objects_device); raise
  * ramcrc_ctx_reserve and retry.  The host entry points (ramcrc_batch_host,

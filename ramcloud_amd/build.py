@@ -6,6 +6,7 @@ The library is plain C ABI (include/ramcrc.h); torch is not linked.  The .so
 lands in ramcloud_amd/lib/ (git-ignored, shipped to the GPU box with the
 snapshot).
 """
+import hashlib
 import os
 import shutil
 import subprocess
@@ -19,7 +20,7 @@ LIB = os.path.join(LIBDIR, "libramcrc.so")
 ARCH = "gfx950"
 
 SOURCES = ["ramcrc_device.hip", "ramcrc_host.cc", "ramcrc_shard.hip", "ramcrc_fill.hip"]
-HEADERS = ["gf2.h", "walk_rules.h"]
+HEADERS = ["gf2.h", "walk_rules.h", "shard_plan.h"]
 
 
 def hipcc():
@@ -29,14 +30,47 @@ def hipcc():
     raise RuntimeError("hipcc not found: the MI355X build needs ROCm")
 
 
-def _stale():
-    if not os.path.exists(LIB):
-        return True
-    t = os.path.getmtime(LIB)
+SHA_MARKER = b"src_sha="
+
+
+def _deps():
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
     deps.append(os.path.join(ROOT, "include", "ramcrc.h"))
     deps.append(os.path.abspath(__file__))
-    return any(os.path.getmtime(d) > t for d in deps)
+    return deps
+
+
+def source_sha(defines=()):
+    """sha256 (first 16 hex digits) of every source, header and compile flag
+    the library is built from.  Compiled into the library (ramcrc_build_info
+    reports it) and read back from the .so to decide staleness, so a shipped
+    library can be tied to the tree it came from."""
+    h = hashlib.sha256()
+    for d in _deps():
+        h.update(os.path.relpath(d, ROOT).encode() + b"\0")
+        with open(d, "rb") as f:
+            h.update(f.read())
+    for d in defines:
+        h.update(b"-D" + d.encode() + b"\0")
+    return h.hexdigest()[:16]
+
+
+def built_sha(path=LIB):
+    """The source hash embedded in a built library, or None."""
+    try:
+        with open(path, "rb") as f:
+            blob = f.read()
+    except OSError:
+        return None
+    i = blob.find(b"ramcrc gfx950 " + SHA_MARKER)
+    if i < 0:
+        return None
+    i += len(b"ramcrc gfx950 " + SHA_MARKER)
+    return blob[i:i + 16].decode("ascii", "replace")
+
+
+def _stale():
+    return built_sha(LIB) != source_sha()
 
 
 def _compile(out, defines=(), verbose=False):
@@ -46,6 +80,7 @@ def _compile(out, defines=(), verbose=False):
            "-fconstexpr-steps=1000000000", "-Wall", "-Wno-unused-function",
            "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
     cmd += ["-D" + d for d in defines]
+    cmd += [f'-DRAMCRC_SRC_SHA="{source_sha(defines)}"']
     cmd += [os.path.join(CSRC, s) for s in SOURCES]
     cmd += ["-ldl", "-o", tmp]
     if verbose:

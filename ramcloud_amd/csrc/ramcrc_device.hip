@@ -161,6 +161,10 @@ constexpr uint32_t kBinOff = kXinvOff + 512;              // k_entries: bin tabl
 constexpr uint32_t kLdsEntries = kBinOff + 4096;          // 152064 B
 static_assert(kLdsEntries <= 160 * 1024, "LDS budget");
 static_assert(kLdsChunks <= 160 * 1024, "LDS budget");
+#define RAMCRC_LDS_CHUNKS 159744    // reported by ramcrc_build_info
+#define RAMCRC_LDS_ENTRIES 152064
+static_assert(kLdsChunks == RAMCRC_LDS_CHUNKS && kLdsEntries == RAMCRC_LDS_ENTRIES,
+              "build_info LDS sizes");
 
 // LDS table fills.  Every thread issues all of its global loads before its
 // first LDS store, so a fill costs about one L2 round trip instead of one per
@@ -451,15 +455,24 @@ __device__ __forceinline__ uint64_t chunk_count(uint64_t S, uint64_t E, uint32_t
     return ((E - 1) >> cshift) - (S >> cshift) + 1;
 }
 
+// Context status word (ramcrc_ctx_status / ramcrc_ctx_check).
+constexpr uint32_t kStatusRefused = 1u;   // this launch's chunk plan overflowed (k_chunks)
+constexpr uint32_t kStatusSticky = 2u;    // some launch wrote no outputs since the last check
+constexpr uint32_t kStatusBins = 4u;      // a binned launch found its layout inconsistent
+
 struct Plan {
-    uint64_t* local;       // per entry: exclusive prefix of chunk counts within its group
+    uint64_t* local;      // per entry: exclusive prefix of chunk counts within its group
     uint64_t* group_pref;  // per group of kThreads entries, exclusive prefix; [ngroups] = total
     uint64_t ngroups;
     uint32_t* partials;
     uint64_t partials_cap;
     uint32_t* status;      // bit 0: this launch's partials overflow; bit 1: sticky (ramcrc_ctx_check)
     unsigned long long* ticket;   // chunk dequeue counter; zero between launches
+    const uint32_t* nlarge;       // nullable: large buffers counted by this sequence's
+                                  // k_bin_count; 0 -> every plan kernel exits at once
 };
+
+__device__ __forceinline__ bool plan_empty(const Plan& pl) { return pl.nlarge && *pl.nlarge == 0; }
 
 __device__ __forceinline__ bool is_large(uint64_t len) { return len >= kLargeMin; }
 
@@ -605,6 +618,8 @@ template <int kMode>
 __global__ __launch_bounds__(kThreads, 1) void k_chunks(BatchDesc d, Plan pl, uint64_t per_seg)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsChunks];
+    if (kMode != kSegAligned && plan_empty(pl))
+        return;   // no buffer of this batch is large: skip the table fill too
     fill_replicated(lds, g_tab.stride_large);
     fill_plain(lds, kCombOff, &g_tab.comb[0].t[0][0], 7 * 1024);
     __syncthreads();
@@ -702,8 +717,8 @@ __global__ __launch_bounds__(256) void k_combine(BatchDesc d, Plan pl, uint64_t 
     const uint64_t wave = uint64_t(blockIdx.x) * (256 / kWaveSize) + threadIdx.x / kWaveSize;
     if (blockIdx.x == 0 && threadIdx.x == 0)
         *pl.ticket = 0;   // k_chunks of this launch is complete (same stream)
-    if (kMode != kSegAligned && ((*pl.status) & 1u))
-        return;   // k_chunks refused the launch (partials overflow)
+    if (kMode != kSegAligned && (plan_empty(pl) || ((*pl.status) & kStatusRefused)))
+        return;   // nothing large, or k_chunks refused the launch (partials overflow)
     const uint64_t n = entry_count<kMode>(d);
     if (!kWide) {
         if (wave >= n)
@@ -785,14 +800,28 @@ constexpr uint32_t kTinyRow0 = 3;            // tiny phase: row of distance m is
 constexpr uint32_t kLdsTiny = 132 * 1024;    // tiny phase: X^m(byte), m = -3..128
 static_assert(kLdsTiny <= kLdsEntries, "k_entries' LDS holds the tiny phase's table");
 
+// The counters a binning sequence (k_bin_count -> k_bin_scatter -> k_entries)
+// accumulates come in two copies selected by the sequence's parity: sequence
+// p counts into copy p while its k_bin_count zeroes copy p ^ 1 for the next
+// sequence.  The host flips the parity only once k_bin_count is enqueued, so a
+// sequence abandoned after that point (a failed later launch) leaves the next
+// one a clean copy; nothing depends on a later kernel of the same sequence
+// having run.  k_entries re-checks the layout against what the scatter wrote
+// (cursor == count for every bin) before it touches a sorted slot.
+struct BinCounters {
+    uint64_t cursor[kNB];     // scatter cursors, relative to start
+    uint32_t hist[kNB];       // entry counts
+    uint32_t kobs[kNB];       // observed max steps (log-scale bins)
+    uint32_t nlarge;          // large buffers the count pass left to k_chunks (skip_large)
+    uint32_t pad_[3];
+};
+
 struct BinTable {
     uint64_t start[kNB];      // first sorted slot of the bin (multiple of 8)
     uint64_t count[kNB];      // entries in the bin
     uint64_t items[kNB + 1];  // exclusive prefix of octets * kmax: work units
-    uint64_t cursor[kNB];     // scatter cursors, relative to start; zero between launches
     uint64_t kcost[kNB];      // steps charged per octet of the bin (observed max)
-    uint32_t hist[kNB];       // entry counts; zero between launches
-    uint32_t kobs[kNB];       // observed max steps (log-scale bins); zero between launches
+    BinCounters ctr[2];       // per parity; copy p ^ 1 is zeroed by sequence p's k_bin_count
 };
 
 struct Sorted {
@@ -800,6 +829,9 @@ struct Sorted {
     u32x4* desc;       // {S lo, S hi, E lo, E hi} per sorted slot
     uint32_t* idx;     // original index; kNoIdx for padding slots
     uint32_t* init;    // initial state per sorted slot (when the batch has one)
+    uint32_t* status;  // context status word (bit 2: inconsistent bin layout)
+    uint64_t cap;      // sorted slots allocated
+    uint32_t par;      // counter copy of this sequence
 };
 
 // First window of an entry in k_entries: its 128-byte line, so that every
@@ -873,8 +905,23 @@ template <int kMode>
 __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, int skip_large)
 {
     __shared__ uint32_t h[kNB], kmx[kNB];
+    __shared__ uint32_t nlarge;
+    BinCounters& ctr = so.bt->ctr[so.par];
+    if (blockIdx.x == 0) {
+        // the next sequence's counters (see BinCounters)
+        BinCounters& nx = so.bt->ctr[so.par ^ 1];
+        for (int t = threadIdx.x; t < kNB; t += blockDim.x) {
+            nx.cursor[t] = 0;
+            nx.hist[t] = 0;
+            nx.kobs[t] = 0;
+        }
+        if (threadIdx.x == 0)
+            nx.nlarge = 0;
+    }
     for (int t = threadIdx.x; t < kNB; t += blockDim.x)
         h[t] = kmx[t] = 0;
+    if (threadIdx.x == 0)
+        nlarge = 0;
     __syncthreads();
     const uint64_t tile = uint64_t(blockDim.x) * kBinPer;
     const uint64_t n = entry_count<kMode>(d);
@@ -887,23 +934,32 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
             S[q] = E[q] = 0;
             act[q] = i < n && buffer_range<kMode>(d, i, S[q], E[q]);
         }
+        uint32_t big = 0;
 #pragma unroll
         for (int q = 0; q < kBinPer; q++) {
-            const bool active = act[q] && !(skip_large && is_large(E[q] - S[q]));
+            const bool large = skip_large && is_large(E[q] - S[q]);
+            big += act[q] && large;
+            const bool active = act[q] && !large;
             const int b = active ? bin_of(S[q], E[q]) : 0;
             if (active && b > 32)
                 atomicMax(&kmx[b], uint32_t(entry_steps(S[q], E[q])));
             uint32_t unused;
             wave_bin_add(h, b, active, unused);
         }
+        if (__ballot(big != 0)) {   // rare: large buffers are few
+            if (big)
+                atomicAdd(&nlarge, big);
+        }
     }
     __syncthreads();
     for (int t = threadIdx.x; t < kNB; t += blockDim.x) {
         if (h[t])
-            atomicAdd(&so.bt->hist[t], h[t]);
+            atomicAdd(&ctr.hist[t], h[t]);
         if (kmx[t])
-            atomicMax(&so.bt->kobs[t], kmx[t]);
+            atomicMax(&ctr.kobs[t], kmx[t]);
     }
+    if (threadIdx.x == 0 && nlarge)
+        atomicAdd(&ctr.nlarge, nlarge);
 }
 
 // Bin layout from the histogram, computed by every k_bin_scatter workgroup
@@ -917,15 +973,19 @@ struct BinScratch {
     uint64_t wpos[4], witem[4];
 };
 
-__device__ __forceinline__ void bin_layout(const Sorted& so, BinScratch& sc, bool publish)
+// Returns false (uniformly) when the histogram asks for more sorted slots
+// than are allocated -- possible only with a corrupted histogram; the layout
+// is then published empty, the status bit set, and nothing is scattered.
+__device__ __forceinline__ bool bin_layout(const Sorted& so, BinScratch& sc, bool publish)
 {
     BinTable* bt = so.bt;
+    const BinCounters& ctr = bt->ctr[so.par];
     const int b = threadIdx.x, lane = b & 63, w = b >> 6;
     uint64_t cnt = 0, kc = 0, ps = 0, is = 0, pos_c = 0, item_c = 0;
     if (b < 256) {
         if (b < kNB) {
-            cnt = bt->hist[b];
-            const uint32_t ko = bt->kobs[b];
+            cnt = ctr.hist[b];
+            const uint32_t ko = ctr.kobs[b];
             kc = b <= 32 ? uint64_t(b == 0 ? 1 : b) : (ko ? ko : bin_kmax(b));
         }
         const uint64_t oct = (cnt + kG - 1) / kG;
@@ -948,23 +1008,29 @@ __device__ __forceinline__ void bin_layout(const Sorted& so, BinScratch& sc, boo
         }
     }
     __syncthreads();
+    const bool ok = sc.wpos[0] + sc.wpos[1] + sc.wpos[2] + sc.wpos[3] <= so.cap;
     if (b < kNB) {
         uint64_t pb = 0, ib = 0;
         for (int j = 0; j < w; j++) {
             pb += sc.wpos[j];
             ib += sc.witem[j];
         }
-        const uint64_t start = pb + ps - pos_c, items = ib + is - item_c;
+        const uint64_t start = ok ? pb + ps - pos_c : 0, items = ok ? ib + is - item_c : 0;
         sc.start[b] = start;
-        sc.count[b] = cnt;
+        sc.count[b] = ok ? cnt : 0;
         if (publish) {
             bt->start[b] = start;
-            bt->count[b] = cnt;
+            bt->count[b] = ok ? cnt : 0;
             bt->items[b] = items;
             bt->kcost[b] = kc + kOctetCost;
             if (b == kNB - 1)
-                bt->items[kNB] = items + item_c;
+                bt->items[kNB] = ok ? items + item_c : 0;
         }
+    }
+    if (!ok) {
+        if (publish && threadIdx.x == 0)
+            atomicOr(so.status, kStatusSticky | kStatusBins);
+        return false;
     }
     __syncthreads();
     if (publish) {
@@ -978,6 +1044,7 @@ __device__ __forceinline__ void bin_layout(const Sorted& so, BinScratch& sc, boo
             }
         }
     }
+    return true;
 }
 
 template <int kMode>
@@ -988,7 +1055,9 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter(BatchDesc d, Sorted so
     __shared__ BinScratch sc;
     for (int t = threadIdx.x; t < kNB; t += blockDim.x)
         cnt[t] = 0;
-    bin_layout(so, sc, blockIdx.x == 0);
+    if (!bin_layout(so, sc, blockIdx.x == 0))
+        return;   // corrupted histogram: nothing is scattered, k_entries refuses
+    unsigned long long* cursor = reinterpret_cast<unsigned long long*>(so.bt->ctr[so.par].cursor);
     const uint64_t tile = uint64_t(blockDim.x) * kBinPer;
     const uint64_t n = entry_count<kMode>(d);
     for (uint64_t t0 = uint64_t(blockIdx.x) * tile; t0 < n; t0 += uint64_t(gridDim.x) * tile) {
@@ -1015,17 +1084,18 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter(BatchDesc d, Sorted so
         __syncthreads();
         for (int t = threadIdx.x; t < kNB; t += blockDim.x)
             if (cnt[t]) {
-                base[t] = sc.start[t] +
-                          atomicAdd(reinterpret_cast<unsigned long long*>(&so.bt->cursor[t]),
-                                    (unsigned long long)cnt[t]);
+                base[t] = atomicAdd(&cursor[t], (unsigned long long)cnt[t]);
                 cnt[t] = 0;
             }
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < kBinPer; q++) {
-            if (b[q] >= 0) {
+            // a slot past the bin's count (a histogram that disagrees with
+            // this pass) is not written; the cursor still counts it, so
+            // k_entries sees cursor != count and refuses the launch
+            if (b[q] >= 0 && base[b[q]] + lp[q] < sc.count[b[q]]) {
                 const uint64_t i = t0 + uint64_t(q) * blockDim.x + threadIdx.x;
-                const uint64_t pos = base[b[q]] + lp[q];
+                const uint64_t pos = sc.start[b[q]] + base[b[q]] + lp[q];
                 so.desc[pos] = u32x4{uint32_t(S[q]), uint32_t(S[q] >> 32), uint32_t(E[q]),
                                      uint32_t(E[q] >> 32)};
                 so.idx[pos] = uint32_t(i);
@@ -1151,10 +1221,13 @@ __device__ __forceinline__ void static_for8(F&& f)
 }
 
 // The first phase of k_entries; lds holds the position table (kLdsTiny bytes).
-__device__ __forceinline__ void tiny_run(const BatchDesc& d, const Sorted& so, uint8_t* lds)
+// Returns false (uniformly) when `bad` is set in any thread of the block: the
+// bin layout disagrees with the scatter, and no slot has been dereferenced.
+__device__ __forceinline__ bool tiny_run(const BatchDesc& d, const Sorted& so, uint8_t* lds,
+                                         bool bad)
 {
     if (so.bt->start[2] == so.bt->start[0])
-        return;   // no entry of at most one window (uniform: every wave exits)
+        return true;   // no entry of at most one window (uniform: every wave exits)
     const int lane = threadIdx.x & (kWaveSize - 1);
     const int gl = lane & 7;
     const uint64_t wave = uint64_t(blockIdx.x) * kEntWaves +
@@ -1204,7 +1277,8 @@ __device__ __forceinline__ void tiny_run(const BatchDesc& d, const Sorted& so, u
     // (issuing the first round's windows before the table fill was 1-2 %
     // slower: the fill's loads queue behind them)
     fill_plain(lds, 0, &g_tab.pos[0][0], 132 * 256);
-    __syncthreads();
+    if (__syncthreads_or(bad))
+        return false;
     u32x4 wc[8];
     uint32_t gc[8], sc;
     issue(o0, wc, gc, sc);
@@ -1298,6 +1372,7 @@ __device__ __forceinline__ void tiny_run(const BatchDesc& d, const Sorted& so, u
             gc[q] = gn[q];
         }
     }
+    return true;
 }
 
 // The tiny phase with conflict-free table lookups (RAMCRC_TINY_CF).  The
@@ -1313,11 +1388,12 @@ __device__ __forceinline__ void tiny_run(const BatchDesc& d, const Sorted& so, u
 // outside the entry are masked to 0 and complemented to column 255, whose
 // rows, and the 128 words after the table, are zero; so no zero rows and
 // no clamps are needed.  Round structure, descriptor ownership and the init
-// fold are those of tiny_run.
-__device__ __forceinline__ void tiny_run_cf(const BatchDesc& d, const Sorted& so, uint8_t* lds)
+// fold are those of tiny_run, and so is the return value.
+__device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so, uint8_t* lds,
+                                            bool bad)
 {
     if (so.bt->start[2] == so.bt->start[0])
-        return;   // no entry of at most one window (uniform: every wave exits)
+        return true;   // no entry of at most one window (uniform: every wave exits)
     const int lane = threadIdx.x & (kWaveSize - 1);
     const uint32_t gl = uint32_t(lane) & 7;
     const uint32_t g4 = (uint32_t(lane) >> 3) & 3;
@@ -1395,7 +1471,8 @@ __device__ __forceinline__ void tiny_run_cf(const BatchDesc& d, const Sorted& so
     uint64_t r = wave;
     TinyOwn o0 = load_own(r), o1 = load_own(r + nwaves);
     fill_plain(lds, 0, g_tab.post, 256 * 128 + 128);
-    __syncthreads();
+    if (__syncthreads_or(bad))
+        return false;
     u32x4 wc[8];
     uint32_t gc[8], sc;
     issue(o0, wc, gc, sc);
@@ -1475,6 +1552,7 @@ __device__ __forceinline__ void tiny_run_cf(const BatchDesc& d, const Sorted& so
             gc[q] = gn[q];
         }
     }
+    return true;
 }
 
 // Entries of two or more 128-byte steps (bins >= 2).  One octet (8 entries,
@@ -1667,6 +1745,10 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
             }
             const uint32_t Koct = __builtin_amdgcn_readfirstlane(kmax32);
             const uint32_t Kmin = __builtin_amdgcn_readfirstlane(kmin32);   // >= 2
+            if (Koct == 0)
+                continue;   // an octet of padding slots only: none in a consistent layout
+                            // (each bin's last octet holds >= 1 entry), but Kmin - 1
+                            // would bound the interior loop at 2^32 steps
             const uint32_t kt0 = Kmin - 1;   // first tail step (>= 1)
             const uint64_t safe = steps ? A : dummy;
 
@@ -1788,22 +1870,32 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
 __global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc d, Sorted so)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsEntries];
-    if (blockIdx.x == 0) {
-        // the histogram and cursors of this launch are consumed: zero them
-        // for the next one (stream-ordered; nothing here reads them)
-        for (int t = threadIdx.x; t < kNB; t += blockDim.x) {
-            so.bt->hist[t] = 0;
-            so.bt->kobs[t] = 0;
-            so.bt->cursor[t] = 0;
-        }
-    }
+    // Every bin must hold exactly the entries the scatter placed in it
+    // (cursor == count): then every sorted slot this launch reads was written
+    // by this sequence.  Checked at the first barrier of each phase, before
+    // any slot's contents are used; a mismatch refuses the launch (no output
+    // written, status bits kStatusSticky | kStatusBins, RAMCRC_EINTERNAL from
+    // ramcrc_ctx_check) instead of walking stale slots.
+    const bool bad = threadIdx.x < kNB &&
+                     so.bt->ctr[so.par].cursor[threadIdx.x] != so.bt->count[threadIdx.x];
+    auto refuse = [&]() {
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            atomicOr(so.status, kStatusSticky | kStatusBins);
+    };
 #if RAMCRC_TINY_CF
-    tiny_run_cf(d, so, lds);
+    const bool tiny_ok = tiny_run_cf(d, so, lds, bad);
 #else
-    tiny_run(d, so, lds);
+    const bool tiny_ok = tiny_run(d, so, lds, bad);
 #endif
-    if (so.bt->items[2] == so.bt->items[kNB])
-        return;   // every entry is tiny (or large on the batch path)
+    if (!tiny_ok) {
+        refuse();
+        return;
+    }
+    if (so.bt->items[2] == so.bt->items[kNB]) {   // every entry is tiny (or large on the batch path)
+        if (__syncthreads_or(bad))
+            refuse();
+        return;
+    }
     __syncthreads();   // the position table is dead: refill the LDS
     fill_replicated(lds, g_tab.stride_small);
     fill_plain(lds, kX4Off, &g_tab.comb[0].t[0][0], 4 * 1024);
@@ -1818,7 +1910,10 @@ __global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc 
             s_cost[t] = uint32_t(so.bt->kcost[t]);
         }
     }
-    __syncthreads();
+    if (__syncthreads_or(bad)) {
+        refuse();
+        return;
+    }
     entries_run<true>(d, so, lds);
     entries_run<false>(d, so, lds);
 }
@@ -1828,6 +1923,8 @@ template <int kMode>
 __global__ __launch_bounds__(kThreads) void k_plan_count(BatchDesc d, Plan pl)
 {
     __shared__ uint64_t wsum[kWavesPerGroup];
+    if (plan_empty(pl))
+        return;   // no large buffer: nothing reads local[] / group_pref[] of this launch
     const uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
     uint64_t c = 0;
     if (i < entry_count<kMode>(d)) {   // local[] is still written for every i < d.n
@@ -1864,8 +1961,15 @@ __global__ __launch_bounds__(kThreads) void k_plan_scan(Plan pl)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     if (threadIdx.x == 0) {
         carry_s = 0;
-        *pl.status &= ~1u;   // stream-ordered before this launch's k_chunks (bit 1 stays)
+        // stream-ordered before this launch's k_chunks; atomic so that a
+        // sticky bit set concurrently by another stream's launch survives
+        atomicAnd(pl.status, ~kStatusRefused);
         *pl.ticket = 0;
+    }
+    if (plan_empty(pl)) {
+        if (threadIdx.x == 0)
+            pl.group_pref[pl.ngroups] = 0;
+        return;
     }
     __syncthreads();
     for (uint64_t base = 0; base < pl.ngroups; base += kThreads) {
@@ -1893,6 +1997,21 @@ __global__ __launch_bounds__(kThreads) void k_plan_scan(Plan pl)
     }
     if (threadIdx.x == 0)
         pl.group_pref[pl.ngroups] = carry_s;
+}
+
+// Test hook (RAMCRC_OPT_TEST_DIRTY_BINS): corrupt the histogram of a binning
+// sequence between its count and scatter passes, as a stale histogram would.
+__global__ void k_test_dirty_bins(BinTable* bt, uint32_t par, uint32_t bin, uint32_t add)
+{
+    if (bin < kNB)
+        bt->ctr[par].hist[bin] += add;
+}
+
+// ramcrc_ctx_check: take the sticky bits (1, 2) atomically; the old word goes
+// to status[1] for the host to read.
+__global__ void k_status_take(uint32_t* status)
+{
+    status[1] = atomicAnd(status, ~(kStatusSticky | kStatusBins));
 }
 
 // ------------------------------------------------------------ host side
@@ -1939,6 +2058,9 @@ struct ramcrc_ctx {
     uint32_t* status = nullptr;
     // small-entry binning
     BinTable* bins = nullptr;
+    uint32_t bin_par = 0;   // counter copy of the next binning sequence (BinCounters)
+    int fail_after_count = 0;   // RAMCRC_OPT_TEST_FAIL_AFTER_COUNT: abandon N sequences
+    uint32_t dirty_bins = 0;    // RAMCRC_OPT_TEST_DIRTY_BINS: bin << 16 | count, once
     u32x4* sdesc = nullptr;
     uint32_t* sidx = nullptr;
     uint32_t* sinit = nullptr;
@@ -2114,25 +2236,54 @@ int reserve_sorted(ramcrc_ctx* c, uint64_t n)
     return RAMCRC_OK;
 }
 
-// Small-entry path: bin by step count, scatter into bin order, scan.
+// Small-entry path: bin by step count, scatter into bin order, scan.  A
+// binning sequence is k_bin_count (bin_begin) ... k_bin_scatter, k_entries
+// (bin_finish); the planned path runs its chunk kernels in between, so that
+// they can exit at once when the count pass found no large buffer.
+uint64_t bin_grid(const ramcrc_ctx* c, uint64_t n)
+{
+    // One tile per workgroup up to kBinWgsPerCu workgroups per CU: the binning
+    // passes are latency-bound loads of 16 B per entry, and one 4-wave
+    // workgroup per CU walking its tiles in turn kept one tile in flight.
+    uint64_t grid = (n + uint64_t(kThreads) * kBinPer - 1) / (uint64_t(kThreads) * kBinPer);
+    if (grid > uint64_t(c->ncu) * kBinWgsPerCu)
+        grid = uint64_t(c->ncu) * kBinWgsPerCu;
+    return grid;
+}
+
 template <int kMode>
-int launch_binned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_large)
+int bin_begin(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_large, Sorted* so)
 {
     if (d.n >= (1ull << 32))
         return RAMCRC_EINVAL;   // sorted slots keep 32-bit entry indices
     int rc = reserve_sorted(c, d.n);
     if (rc)
         return rc;
-    Sorted so{c->bins, c->sdesc, c->sidx, c->sinit};
-    // One tile per workgroup up to kBinWgsPerCu workgroups per CU: the binning
-    // passes are latency-bound loads of 16 B per entry, and one 4-wave
-    // workgroup per CU walking its tiles in turn kept one tile in flight.
-    uint64_t grid = (d.n + uint64_t(kThreads) * kBinPer - 1) / (uint64_t(kThreads) * kBinPer);
-    if (grid > uint64_t(c->ncu) * kBinWgsPerCu)
-        grid = uint64_t(c->ncu) * kBinWgsPerCu;
-    hipLaunchKernelGGL(k_bin_count<kMode>, dim3(grid), dim3(kThreads), 0, s, d, so, skip_large);
+    *so = Sorted{c->bins, c->sdesc, c->sidx, c->sinit, c->status, c->sorted_cap, c->bin_par};
+    (void)hipGetLastError();   // clear a stale error: the next one is this launch's
+    hipLaunchKernelGGL(k_bin_count<kMode>, dim3(bin_grid(c, d.n)), dim3(kThreads), 0, s, d, *so,
+                       skip_large);
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_bin_scatter<kMode>, dim3(grid), dim3(kThreads), 0, s, d, so, skip_large);
+    // enqueued: it zeroes the other copy, which the next sequence uses
+    c->bin_par ^= 1u;
+    return RAMCRC_OK;
+}
+
+template <int kMode>
+int bin_finish(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_large, const Sorted& so)
+{
+    if (c->fail_after_count > 0) {   // test hook: a failure after k_bin_count
+        c->fail_after_count--;
+        return RAMCRC_EHIP;
+    }
+    if (c->dirty_bins) {   // test hook: a stale histogram
+        hipLaunchKernelGGL(k_test_dirty_bins, dim3(1), dim3(1), 0, s, c->bins, so.par,
+                           uint32_t(c->dirty_bins >> 16), uint32_t(c->dirty_bins & 0xFFFF));
+        c->dirty_bins = 0;
+        HIPCHK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_bin_scatter<kMode>, dim3(bin_grid(c, d.n)), dim3(kThreads), 0, s, d, so,
+                       skip_large);
     HIPCHK(hipGetLastError());
     {
         ScanTimer t(c, s);
@@ -2143,9 +2294,24 @@ int launch_binned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_lar
 }
 
 template <int kMode>
+int launch_binned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_large)
+{
+    Sorted so;
+    int rc = bin_begin<kMode>(c, d, s, skip_large, &so);
+    if (rc)
+        return rc;
+    return bin_finish<kMode>(c, d, s, skip_large, so);
+}
+
+template <int kMode>
 int launch_planned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s)
 {
+    Sorted so;
+    int rc = bin_begin<kMode>(c, d, s, 1, &so);
+    if (rc)
+        return rc;
     Plan pl = make_plan(c, d.n);
+    pl.nlarge = &so.bt->ctr[so.par].nlarge;
     hipLaunchKernelGGL(k_plan_count<kMode>, dim3(pl.ngroups), dim3(kThreads), 0, s, d, pl);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(kThreads), 0, s, pl);
@@ -2162,7 +2328,7 @@ int launch_planned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s)
         hipLaunchKernelGGL((k_combine<kMode, false>), dim3((d.n + 3) / 4), dim3(256), 0, s, d, pl,
                            uint64_t(0));
     HIPCHK(hipGetLastError());
-    return launch_binned<kMode>(c, d, s, 1);
+    return bin_finish<kMode>(c, d, s, 1, so);
 }
 
 // ------------------------------------------------------------ segment walk
@@ -3699,14 +3865,28 @@ const char* ramcrc_strerror(int code)
     case RAMCRC_ENODEV: return "no usable device";
     case RAMCRC_ERCCL: return "rccl failure";
     case RAMCRC_EREFUSED: return "launch refused: chunk scratch too small (ramcrc_ctx_reserve)";
+    case RAMCRC_EINTERNAL: return "launch refused: inconsistent small-entry bin layout";
     default: return "unknown error";
     }
 }
 
+#ifndef RAMCRC_SRC_SHA
+#define RAMCRC_SRC_SHA "unknown"
+#endif
+#define RAMCRC_STR2(x) #x
+#define RAMCRC_STR(x) RAMCRC_STR2(x)
+
 const char* ramcrc_build_info(void)
 {
-    return "ramcrc gfx950: chunk=256KiB block=1KiB waves/WG=16 unroll=8 lds_chunks=159744 "
-           "lds_entries=136192 large_min=64KiB";
+    // src_sha: sha256 of the sources the library was built from (build.py),
+    // the same marker build.py reads back to decide staleness
+    return "ramcrc gfx950 src_sha=" RAMCRC_SRC_SHA
+           " chunk=" RAMCRC_STR(RAMCRC_CHUNK_SHIFT) "..20 (adaptive: largest giving every wave two chunks)"
+           " block=1KiB waves/WG=16 unroll=" RAMCRC_STR(RAMCRC_UNROLL)
+           " lds_chunks=" RAMCRC_STR(RAMCRC_LDS_CHUNKS) " lds_entries=" RAMCRC_STR(RAMCRC_LDS_ENTRIES)
+           " entries: waves=" RAMCRC_STR(RAMCRC_ENT_WAVES) " smallk=" RAMCRC_STR(RAMCRC_SMALLK)
+           " pu=" RAMCRC_STR(RAMCRC_PU) " tiny_cf=" RAMCRC_STR(RAMCRC_TINY_CF)
+           " large_min=64KiB part_shift=" RAMCRC_STR(RAMCRC_PART_SHIFT);
 }
 
 int ramcrc_ctx_create(int device, ramcrc_ctx** out)
@@ -3802,6 +3982,16 @@ int ramcrc_ctx_set_option(ramcrc_ctx* c, int option, int64_t value)
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     switch (option) {
     case RAMCRC_OPT_SERIAL_WALK: c->serial_walk = value != 0; return RAMCRC_OK;
+    case RAMCRC_OPT_TEST_FAIL_AFTER_COUNT:
+        if (value < 0 || value > 1000)
+            return RAMCRC_EINVAL;
+        c->fail_after_count = int(value);
+        return RAMCRC_OK;
+    case RAMCRC_OPT_TEST_DIRTY_BINS:
+        if (value < 0 || value > 0xFFFFFFFFll)
+            return RAMCRC_EINVAL;
+        c->dirty_bins = uint32_t(value);
+        return RAMCRC_OK;
     case RAMCRC_OPT_WALK_PART_SHIFT:
         if (value != 0 && (value < kPartShiftMin || value > 20))
             return RAMCRC_EINVAL;
@@ -3892,14 +4082,21 @@ int ramcrc_ctx_check(ramcrc_ctx* c, void* stream)
         return RAMCRC_EINVAL;
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     DeviceGuard g(c->device);
-    HIPCHK(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    HIPCHK(hipStreamSynchronize(s));
     uint32_t st = 0;
     HIPCHK(hipMemcpy(&st, c->status, sizeof(uint32_t), hipMemcpyDeviceToHost));
-    if (!(st & 2u))
+    if (!(st & kStatusSticky))
         return RAMCRC_OK;
-    const uint32_t cleared = st & ~3u;
-    HIPCHK(hipMemcpy(c->status, &cleared, sizeof(uint32_t), hipMemcpyHostToDevice));
-    return RAMCRC_EREFUSED;
+    // take the sticky bits with one device atomic: a bit another stream's
+    // launch sets meanwhile is either taken here or stays for the next check
+    hipLaunchKernelGGL(k_status_take, dim3(1), dim3(1), 0, s, c->status);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipMemcpy(&st, c->status + 1, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (st & kStatusBins)
+        return RAMCRC_EINTERNAL;
+    return (st & kStatusSticky) ? RAMCRC_EREFUSED : RAMCRC_OK;
 }
 
 int ramcrc_segments_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_bytes, uint64_t nseg,

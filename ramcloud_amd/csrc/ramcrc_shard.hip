@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "ramcrc.h"
+#include "shard_plan.h"
 
 namespace {
 
@@ -102,18 +103,14 @@ int rccl_fail(const Rccl* r, ncclResult_t e, const char* what)
             return RAMCRC_EHIP;                   \
     } while (0)
 
-// all[s] = gather[q * width + s - lo_q] for the owner q of segment s.
+// all[s] = gather[gather_index(s)] (shard_plan.h).
 __global__ __launch_bounds__(256) void k_unpad(const uint32_t* gather, uint32_t* all, uint64_t nseg,
-                                               uint64_t width, uint64_t base, uint64_t rem)
+                                               uint64_t nranks)
 {
     const uint64_t s = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (s >= nseg)
         return;
-    // owners 0 .. rem-1 hold base + 1 segments, the others base
-    const uint64_t big = rem * (base + 1);
-    const uint64_t q = s < big ? s / (base + 1) : rem + (s - big) / base;
-    const uint64_t lo = q < rem ? q * (base + 1) : big + (q - rem) * base;
-    all[s] = gather[q * width + (s - lo)];
+    all[s] = gather[ramcrc_shard_plan::gather_index(s, nseg, nranks)];
 }
 
 struct Local {
@@ -128,6 +125,7 @@ struct Local {
     uint64_t all_cap = 0;
     uint64_t last_nseg = 0;
     bool last_internal = false;
+    int failed = 0;               // a step's failure after its collective was enqueued
 };
 
 struct DevGuard {
@@ -187,6 +185,79 @@ int finish_create(ramcrc_shard* sh)
     return RAMCRC_OK;
 }
 
+// The environment of ramcrc_shard_plan::run_step: HIP streams, contexts and RCCL.
+struct StepOps {
+    ramcrc_shard* sh;
+    const Rccl* r;
+    const void* const* d_shard;
+    uint32_t* const* d_all;
+    uint64_t seg_bytes;
+    uint32_t flags;
+
+    uint32_t* recv(int k, bool caller) { return caller ? d_all[k] : sh->local[k].gather; }
+    int check(int k, uint64_t lo, uint64_t hi)
+    {
+        if (hi > lo && !d_shard[k])
+            return RAMCRC_EINVAL;
+        if (d_all && !d_all[k])
+            return RAMCRC_EINVAL;
+        return RAMCRC_OK;
+    }
+    int reserve(int k, uint64_t gather_elems, uint64_t all_elems)
+    {
+        Local& l = sh->local[k];
+        DevGuard g(l.device);
+        l.failed = 0;
+        int rc = gather_elems ? grow(&l.gather, &l.gather_cap, gather_elems) : RAMCRC_OK;
+        if (!rc && all_elems)
+            rc = grow(&l.all, &l.all_cap, all_elems);
+        return rc;
+    }
+    int scan(int k, uint64_t lo, uint64_t hi, bool caller, uint64_t off)
+    {
+        Local& l = sh->local[k];
+        DevGuard g(l.device);
+        return ramcrc_segments_device(l.ctx, d_shard[k], seg_bytes, hi - lo, nullptr,
+                                      recv(k, caller) + off, flags, l.stream);
+    }
+    int poison(int k, bool caller, uint64_t off, uint64_t count)
+    {
+        Local& l = sh->local[k];
+        DevGuard g(l.device);
+        HIPCHK_S(hipMemsetAsync(recv(k, caller) + off, 0xFF, count * sizeof(uint32_t), l.stream));
+        return RAMCRC_OK;
+    }
+    int group_start()
+    {
+        RCCLCHK(r, r->group_start(), "ncclGroupStart");
+        return RAMCRC_OK;
+    }
+    int group_end()
+    {
+        RCCLCHK(r, r->group_end(), "ncclGroupEnd");
+        return RAMCRC_OK;
+    }
+    int all_gather(int k, bool caller, uint64_t off, uint64_t count)
+    {
+        Local& l = sh->local[k];
+        uint32_t* buf = recv(k, caller);
+        RCCLCHK(r, r->all_gather(buf + off, buf, count, ncclUint32, l.comm, l.stream),
+                "ncclAllGather");
+        return RAMCRC_OK;
+    }
+    int unpad(int k, uint64_t nseg, uint64_t nranks)
+    {
+        Local& l = sh->local[k];
+        DevGuard g(l.device);
+        uint32_t* dst = d_all ? d_all[k] : l.all;
+        hipLaunchKernelGGL(k_unpad, dim3((nseg + 255) / 256), dim3(256), 0, l.stream, l.gather,
+                           dst, nseg, nranks);
+        HIPCHK_S(hipGetLastError());
+        return RAMCRC_OK;
+    }
+    void set_failed(int k, int rc) { sh->local[k].failed = rc; }
+};
+
 }  // namespace
 
 extern "C" {
@@ -195,10 +266,7 @@ int ramcrc_shard_range(uint64_t nseg, int nranks, int rank, uint64_t* lo, uint64
 {
     if (nranks < 1 || rank < 0 || rank >= nranks || !lo || !hi)
         return RAMCRC_EINVAL;
-    const uint64_t base = nseg / uint64_t(nranks), rem = nseg % uint64_t(nranks);
-    const uint64_t r = uint64_t(rank);
-    *lo = r * base + (r < rem ? r : rem);
-    *hi = *lo + base + (r < rem ? 1 : 0);
+    ramcrc_shard_plan::range(nseg, uint64_t(nranks), uint64_t(rank), lo, hi);
     return RAMCRC_OK;
 }
 
@@ -354,63 +422,18 @@ int ramcrc_shard_segments(ramcrc_shard* sh, const void* const* d_shard, uint64_t
     if (!r)
         return RAMCRC_ERCCL;
     std::lock_guard<std::mutex> lk(sh->mu);
-    const uint64_t N = uint64_t(sh->nranks);
-    const uint64_t width = (nseg + N - 1) / N;
-    const uint64_t base = nseg / N, rem = nseg % N;
-    if (width == 0) {
-        for (Local& l : sh->local)
-            l.last_nseg = 0;
-        return RAMCRC_OK;
-    }
-    // a uniform split lets the all-gather land directly in the caller's array
-    const bool direct = rem == 0 && d_all;
-    for (size_t k = 0; k < sh->local.size(); k++) {
-        Local& l = sh->local[k];
-        DevGuard g(l.device);
-        uint64_t lo = 0, hi = 0;
-        ramcrc_shard_range(nseg, sh->nranks, l.rank, &lo, &hi);
-        if (hi > lo && !d_shard[k])
-            return RAMCRC_EINVAL;
-        int rc = RAMCRC_OK;
-        if (!direct)
-            rc = grow(&l.gather, &l.gather_cap, width * N);
-        if (!rc && !d_all)
-            rc = grow(&l.all, &l.all_cap, nseg);
-        if (rc)
-            return rc;
-        uint32_t* recv = direct ? d_all[k] : l.gather;
-        rc = ramcrc_segments_device(l.ctx, d_shard[k], seg_bytes, hi - lo, nullptr,
-                                    recv + uint64_t(l.rank) * width, flags, l.stream);
-        if (rc)
-            return rc;
-        l.last_nseg = nseg;
+    const int nlocal = int(sh->local.size());
+    std::vector<int> ranks(nlocal);
+    for (int k = 0; k < nlocal; k++)
+        ranks[k] = sh->local[k].rank;
+    StepOps ops{sh, r, d_shard, d_all, seg_bytes, flags};
+    const int rc = ramcrc_shard_plan::run_step(ops, nlocal, ranks.data(), sh->nranks, nseg,
+                                               d_all != nullptr);
+    for (Local& l : sh->local) {
+        l.last_nseg = rc ? 0 : nseg;
         l.last_internal = !d_all;
     }
-    // one group: a single process driving several ranks must issue their
-    // collectives together (a lone rank's call would block on the others)
-    RCCLCHK(r, r->group_start(), "ncclGroupStart");
-    for (size_t k = 0; k < sh->local.size(); k++) {
-        Local& l = sh->local[k];
-        uint32_t* recv = direct ? d_all[k] : l.gather;
-        ncclResult_t e = r->all_gather(recv + uint64_t(l.rank) * width, recv, width, ncclUint32,
-                                       l.comm, l.stream);
-        if (e != ncclSuccess) {
-            (void)r->group_end();
-            return rccl_fail(r, e, "ncclAllGather");
-        }
-    }
-    RCCLCHK(r, r->group_end(), "ncclGroupEnd");
-    if (!direct) {
-        for (size_t k = 0; k < sh->local.size(); k++) {
-            Local& l = sh->local[k];
-            DevGuard g(l.device);
-            uint32_t* dst = d_all ? d_all[k] : l.all;
-            hipLaunchKernelGGL(k_unpad, dim3((nseg + 255) / 256), dim3(256), 0, l.stream,
-                               l.gather, dst, nseg, width, base, rem);
-            HIPCHK_S(hipGetLastError());
-        }
-    }
-    return RAMCRC_OK;
+    return rc;
 }
 
 int ramcrc_shard_sync(ramcrc_shard* sh)
@@ -430,6 +453,8 @@ int ramcrc_shard_sync(ramcrc_shard* sh)
         int rc = ramcrc_ctx_check(l.ctx, l.stream);
         if (rc)
             return rc;
+        if (l.failed)
+            return l.failed;   // its slots of the last step were poisoned
     }
     return RAMCRC_OK;
 }

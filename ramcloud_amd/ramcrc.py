@@ -20,11 +20,22 @@ _lib = None
 FINALIZE = 1
 
 _ERRORS = {0: "ok", -1: "invalid argument", -2: "out of memory", -3: "HIP error",
-           -4: "no usable device", -5: "RCCL error", -6: "launch refused (scratch too small)"}
+           -4: "no usable device", -5: "RCCL error", -6: "launch refused (scratch too small)",
+           -7: "launch refused (inconsistent bin layout)"}
+
+EINTERNAL = -7
+
+# ramcrc_ctx_set_option options (include/ramcrc.h)
+OPT_SERIAL_WALK = 1
+OPT_WALK_PART_SHIFT = 2
+OPT_TEST_FAIL_AFTER_COUNT = 3
+OPT_TEST_DIRTY_BINS = 4
 
 
 class RamcrcError(RuntimeError):
-    pass
+    def __init__(self, msg, code=None):
+        super().__init__(msg)
+        self.code = code
 
 
 def lib_path():
@@ -109,7 +120,7 @@ def exported_symbols():
 def _check(rc, what):
     if rc != 0:
         msg = lib().ramcrc_strerror(rc).decode()
-        raise RamcrcError(f"{what} failed: {_ERRORS.get(rc, rc)} ({msg})")
+        raise RamcrcError(f"{what} failed: {_ERRORS.get(rc, rc)} ({msg})", rc)
 
 
 def _buf(data):
@@ -267,6 +278,10 @@ class Context:
         """log2 of the parallel walk's part size, 13..20; 0 = the default 64 KiB
         (RAMCRC_OPT_WALK_PART_SHIFT)."""
         _check(lib().ramcrc_ctx_set_option(self._h, 2, int(shift)), "ramcrc_ctx_set_option")
+
+    def set_option(self, option, value):
+        """ramcrc_ctx_set_option (OPT_* above)."""
+        _check(lib().ramcrc_ctx_set_option(self._h, int(option), int(value)), "ramcrc_ctx_set_option")
 
     def set_cus(self, ncu):
         """Size this context's persistent grids for ncu CUs (0 = all): for

@@ -1,0 +1,148 @@
+"""The small-entry binning sequence (k_bin_count -> k_bin_scatter -> k_entries)
+across failed and corrupted launches.
+
+Round 2 recorded a GPU hang in k_entries whose cause was a bin layout that
+disagreed with the slots the scatter had written (stale slots, an octet of
+padding only: the interior loop bound Kmin - 1 then wrapped to 2^32).  The
+counters are now per-sequence copies (BinCounters), flipped only once
+k_bin_count is enqueued, and k_entries refuses a launch whose layout does not
+match what was scattered.  These tests drive exactly those paths through the
+C ABI's test hooks (RAMCRC_OPT_TEST_FAIL_AFTER_COUNT, RAMCRC_OPT_TEST_DIRTY_BINS)
+and check every later call bit-exact against the oracle.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def run(ctx, api, base, offs, lens, init=None, out=None):
+    n = len(offs)
+    if out is None:
+        out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    off_t = dev(np.asarray(offs, dtype=np.uint64).view(np.int64))
+    len_t = dev(np.asarray(lens, dtype=np.uint64).view(np.int64))
+    init_t = None if init is None else dev(np.asarray(init, dtype=np.uint32).view(np.int32))
+    getattr(ctx, api)(base, off_t, len_t, out, init=init_t)
+    return out
+
+
+def host_u32(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy().view(np.uint32)
+
+
+def alignment_case(oracle_mod, seed=4242, with_long=True):
+    host = oracle_mod.splitmix_bytes(seed, 1 << 20)
+    lens = list(range(0, 300, 3)) + ([1023, 1024, 1025, 4095, 4096, 9000] if with_long else [])
+    offs, ls = [], []
+    for s in range(0, 128, 5):
+        for L in lens:
+            offs.append(1024 + s + 128 * ((s * 7 + L) % 64))
+            ls.append(L)
+    rng = np.random.default_rng(seed)
+    init = rng.integers(0, 2 ** 32, len(offs), dtype=np.uint64).astype(np.uint32)
+    return host, offs, ls, init
+
+
+@pytest.fixture()
+def ctx(ramcrc):
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    c = ramcrc.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("api", ["entries", "batch"])
+@pytest.mark.parametrize("fails", [1, 2, 3])
+def test_failed_sequence_then_init_call(ctx, ramcrc, oracle_mod, api, fails):
+    """A sequence abandoned right after its histogram pass (the early return
+    of a failed later launch) must not leak into the next calls -- the
+    round-2 hang was the first call with an initial-state array after such a
+    hand-off."""
+    host, offs, ls, init = alignment_case(oracle_mod)
+    base = dev(host)
+    ctx.set_option(ramcrc.OPT_TEST_FAIL_AFTER_COUNT, fails)
+    for _ in range(fails):
+        with pytest.raises(ramcrc.RamcrcError) as e:
+            run(ctx, api, base, offs, ls, init)
+        assert e.value.code == -3
+    for it in (init, None, init):
+        got = host_u32(run(ctx, api, base, offs, ls, it))
+        want = oracle_mod.entries(host, offs, ls, init=it)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, [(offs[i] % 128, ls[i]) for i in bad[:8]]
+    ctx.check()
+
+
+@pytest.mark.parametrize("api", ["entries", "batch"])
+@pytest.mark.parametrize("bin_, add", [(1, 3), (2, 1), (9, 5), (40, 7), (160, 2)])
+def test_dirty_histogram_is_refused(ctx, ramcrc, oracle_mod, api, bin_, add):
+    """A histogram that disagrees with the scatter (as a stale one would):
+    the launch writes nothing and ramcrc_ctx_check reports RAMCRC_EINTERNAL;
+    the next call is exact."""
+    host, offs, ls, init = alignment_case(oracle_mod, seed=7)
+    base = dev(host)
+    sentinel = torch.full((len(offs),), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    ctx.set_option(ramcrc.OPT_TEST_DIRTY_BINS, (bin_ << 16) | add)
+    run(ctx, api, base, offs, ls, init, out=sentinel)
+    with pytest.raises(ramcrc.RamcrcError) as e:
+        ctx.check()
+    assert e.value.code == ramcrc.EINTERNAL
+    got = host_u32(sentinel)
+    # small entries are not written (large ones on the batch path are k_chunks')
+    small = np.array([L < 65536 for L in ls])
+    assert np.all(got[small] == 0x5A5A5A5A)
+    ctx.check()   # the sticky bits were taken
+    got = host_u32(run(ctx, api, base, offs, ls, init))
+    assert np.array_equal(got, oracle_mod.entries(host, offs, ls, init=init))
+    ctx.check()
+
+
+def test_histogram_past_capacity_is_refused(ramcrc, oracle_mod):
+    """A histogram asking for more sorted slots than the context holds: the
+    scatter writes nothing (no out-of-bounds slot), the launch is refused."""
+    c = ramcrc.Context(0)
+    try:
+        host = oracle_mod.splitmix_bytes(3, 1 << 16)
+        offs = [17 * i for i in range(200)]
+        ls = [100] * 200
+        base = dev(host)
+        sentinel = torch.full((200,), 0x1234, dtype=torch.int32, device="cuda")
+        c.set_option(ramcrc.OPT_TEST_DIRTY_BINS, (1 << 16) | 0xFFFF)
+        run(c, "entries", base, offs, ls, out=sentinel)
+        with pytest.raises(ramcrc.RamcrcError) as e:
+            c.check()
+        assert e.value.code == ramcrc.EINTERNAL
+        assert np.all(host_u32(sentinel) == 0x1234)
+        got = host_u32(run(c, "entries", base, offs, ls))
+        assert np.array_equal(got, oracle_mod.entries(host, offs, ls))
+    finally:
+        c.close()
+
+
+def test_plan_skip_alternating(ctx, oracle_mod):
+    """The batch path skips its chunk kernels when the count pass finds no
+    buffer of >= 64 KiB: alternate batches with and without large buffers (and
+    with and without initial states) on one context."""
+    rng = np.random.default_rng(99)
+    total = 8 << 20
+    host = oracle_mod.splitmix_bytes(11, total)
+    base = dev(host)
+    for k in range(6):
+        big = k % 2 == 1
+        lens = [int(x) for x in rng.integers(0, 5000, 2000)]
+        if big:
+            lens += [65536, 65537, 300000, 1 << 20]
+        offs = [int(rng.integers(0, total - L + 1)) for L in lens]
+        init = None if k % 3 == 0 else rng.integers(0, 2 ** 32, len(lens),
+                                                   dtype=np.uint64).astype(np.uint32)
+        got = host_u32(run(ctx, "batch", base, offs, lens, init))
+        want = oracle_mod.entries(host, offs, lens, init=init)
+        assert np.array_equal(got, want), k
+    ctx.check()
