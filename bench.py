@@ -263,22 +263,39 @@ def cpu_baseline_segments(host, seg_bytes, nseg, gpu_crcs, reps=5):
     }
 
 
-def cpu_baseline_entries(host, offs, lens, gpu_crcs, reps=3):
-    """Crc32C::update per entry (the reference's loop of one call per log
-    entry, src/ObjectManager.cc:659-669) restated in the oracle, 1 thread,
-    plus the bit-exact check of every GPU CRC."""
+def cpu_baseline_entries(host, offs, lens, gpu_crcs, reps=5):
+    """The reference's own intelCrc32C (src/Crc32C.h:39-93; oracle/_ref) once
+    per entry -- the reference's loop of one Crc32C per log entry / object
+    (src/ObjectManager.cc:659-669, src/Object.cc:805-819) -- 1 thread and T
+    threads (blocks of 4096 entries round-robin over pinned threads), best and
+    median of `reps`; the oracle restatement on 1 thread when oracle/_ref was
+    not built.  Also the bit-exact check of every GPU CRC."""
     from oracle import oracle
-    times = []
-    want = None
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        want = oracle.entries(host, offs, lens)
-        times.append(time.perf_counter() - t0)
+    use_ref = oracle.ref_available()
+    info = host_cpu_info()
+    threads = baseline_threads(info) if use_ref else 1
     total = int(lens.sum())
-    return {"value": round(total / min(times) / 1e9, 3), "unit": "GB/s", "cores": 1,
-            "kind": "port",
-            "sample": f"all {lens.size} entries ({total} B), oracle SSE4.2 restatement of "
-                      f"intelCrc32C, one update per entry, best of {reps}",
+    res, want = {}, None
+    for t in sorted({1, threads}):
+        times = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            want = (oracle.ref_entries(host, offs, lens, threads=t) if use_ref
+                    else oracle.entries(host, offs, lens))
+            times.append(time.perf_counter() - t0)
+        res[t] = (total / min(times) / 1e9, total / statistics.median(times) / 1e9)
+    best, median = res[threads]
+    return {"value": round(best, 3), "unit": "GB/s", "cores": threads,
+            "kind": "reference" if use_ref else "port",
+            "sample": (f"all {lens.size} entries ({total} B), one Crc32C per entry, best of {reps} "
+                       f"(median {median:.3f} GB/s); "
+                       + ("RAMCloud intelCrc32C (src/Crc32C.h:39-93) compiled -O3 -msse4.2 from the "
+                          "reference, blocks of 4096 entries round-robin over pinned threads"
+                          if use_ref else "oracle SSE4.2 restatement of intelCrc32C, 1 thread")),
+            "median": round(median, 3),
+            "single_thread_GBs": round(res[1][0], 3),
+            "threads_rule": "min(physical cores, affinity, cgroup cpu.max quota)",
+            "host": info,
             "bit_exact_vs_gpu": bool(np.array_equal(want, gpu_crcs))}
 
 
@@ -549,25 +566,42 @@ def run_entries(args, ranks):
     }
 
 
-def replay_cpu_baseline(host, seg_bytes, certs, nsample):
-    """The restated reference walk + per-object verify (oracle, SSE4.2 CRC) on
-    nsample segments, one thread -- the checksum work of one
-    RecoverSegmentBenchmark replay thread."""
+def replay_cpu_baseline(host, seg_bytes, certs, nsample, reps=3):
+    """The checksum work of RecoverSegmentBenchmark's replay threads
+    (nanobenchmarks/RecoverSegmentBenchmark.cc:90-118) on nsample segments:
+    Segment::checkMetadataIntegrity (the oracle's restated walk) and the
+    replaySegment checks of every record, every CRC byte through the
+    reference's own intelCrc32C (oracle/_ref; the SSE4.2 restatement when it
+    was not built), whole segments round-robin over 1 and T pinned threads,
+    best and median of `reps`."""
     from oracle import oracle
-    t0 = time.perf_counter()
-    bad = 0
-    for i in range(nsample):
-        s = host[i * seg_bytes:(i + 1) * seg_bytes]
-        f, ck, n, table = oracle.check_metadata(s, int(certs[i, 0]), int(certs[i, 1]),
-                                                segment=0, table_cap=seg_bytes // 14 + 1)
-        b, _, _ = oracle.verify_objects(s, seg_bytes, table, 1)
-        bad += b + (0 if f == 1 else 1)
-    dt = time.perf_counter() - t0
-    return {"value": round(nsample * seg_bytes / dt / 1e9, 3), "unit": "GB/s", "cores": 1,
-            "kind": "port",
-            "sample": f"{nsample} x {seg_bytes // MiB} MiB object segments, oracle restatement of "
-                      "Segment::checkMetadataIntegrity + Object::computeChecksum, 1 thread",
-            "all_verified": bad == 0}
+    use_ref = oracle.ref_available()
+    info = host_cpu_info()
+    threads = baseline_threads(info)
+    certs = np.ascontiguousarray(certs, dtype=np.uint32).reshape(-1, 2)
+    res, failed = {}, None
+    for t in sorted({1, threads}):
+        times = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            failed = oracle.replay_mt(host, seg_bytes, nsample, certs, threads=t, use_ref=use_ref)
+            times.append(time.perf_counter() - t0)
+        res[t] = (nsample * seg_bytes / min(times) / 1e9,
+                  nsample * seg_bytes / statistics.median(times) / 1e9)
+    best, median = res[threads]
+    return {"value": round(best, 3), "unit": "GB/s", "cores": threads,
+            "kind": "reference" if use_ref else "port",
+            "sample": (f"{nsample} x {seg_bytes // MiB} MiB object segments, best of {reps} "
+                       f"(median {median:.3f} GB/s): the oracle's restated walk "
+                       "(Segment::checkMetadataIntegrity) + replaySegment checks, every CRC byte "
+                       + ("through RAMCloud intelCrc32C (src/Crc32C.h:39-93) compiled from the reference"
+                          if use_ref else "through the oracle's SSE4.2 restatement")
+                       + ", whole segments round-robin over pinned threads"),
+            "median": round(median, 3),
+            "single_thread_GBs": round(res[1][0], 3),
+            "threads_rule": "min(physical cores, affinity, cgroup cpu.max quota)",
+            "host": info,
+            "all_verified": failed == 0}
 
 
 def _walk_cu_list(ncu, walk_cus):
@@ -859,7 +893,7 @@ def parse_args(argv=None):
     ap.add_argument("--entry-size", type=int, default=0, help="fixed entry length (default: Zipf mix)")
     ap.add_argument("--replay-nseg", type=int, default=512,
                     help="replay config: segments (RecoverSegmentBenchmark: 4096/8)")
-    ap.add_argument("--replay-cpu-sample", type=int, default=16,
+    ap.add_argument("--replay-cpu-sample", type=int, default=64,
                     help="replay config: segments verified by the CPU baseline")
     ap.add_argument("--walk-cus", type=int, default=0,
                     help="replay config: pipeline batches, walking on this many CUs "
@@ -893,11 +927,17 @@ def main():
     json_fd = os.dup(1)
     os.dup2(2, 1)
 
+    from ramcloud_amd import build as rbuild, ramcrc
+    ramcrc.lib()  # fail loudly if the HIP library is missing
+    info = ramcrc.lib().ramcrc_build_info().decode()
+
     def emit(line):
+        # provenance: the source hash compiled into the library that ran, and
+        # whether it matches the sources of this tree
+        line["build_info"] = info
+        line["build_matches_tree"] = rbuild.built_sha(ramcrc.lib_path()) == rbuild.source_sha()
         os.write(json_fd, (json.dumps(line) + "\n").encode())
 
-    from ramcloud_amd import ramcrc
-    ramcrc.lib()  # fail loudly if the HIP library is missing
     if args.config == "host":
         emit(run_host())
         return 0

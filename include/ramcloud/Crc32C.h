@@ -32,18 +32,21 @@
 #define PRIVATE private
 #endif
 
-/// The software path's lookup tables under the reference's names
-/// (src/Crc32C.h:25-34): references into libramcrc's compile-time tables
-/// (ramcrc_slice8_tables), indexed exactly like the reference's arrays.
+/// The software path's lookup tables under the reference's names and types
+/// (src/Crc32C.h:25-34): plain arrays, so objects compiled against the
+/// reference header link against them too.  Defined (generated from the
+/// polynomial at compile time, statically initialised) in
+/// ramcloud_amd/dropin/Crc32C.cc; libramcrc's own copies
+/// (ramcrc_slice8_tables) hold the same values.
 namespace Crc32CSlicingBy8 {
-extern const uint32_t (&crc_tableil8_o32)[256];
-extern const uint32_t (&crc_tableil8_o40)[256];
-extern const uint32_t (&crc_tableil8_o48)[256];
-extern const uint32_t (&crc_tableil8_o56)[256];
-extern const uint32_t (&crc_tableil8_o64)[256];
-extern const uint32_t (&crc_tableil8_o72)[256];
-extern const uint32_t (&crc_tableil8_o80)[256];
-extern const uint32_t (&crc_tableil8_o88)[256];
+extern const uint32_t crc_tableil8_o32[256];
+extern const uint32_t crc_tableil8_o40[256];
+extern const uint32_t crc_tableil8_o48[256];
+extern const uint32_t crc_tableil8_o56[256];
+extern const uint32_t crc_tableil8_o64[256];
+extern const uint32_t crc_tableil8_o72[256];
+extern const uint32_t crc_tableil8_o80[256];
+extern const uint32_t crc_tableil8_o88[256];
 }  // namespace Crc32CSlicingBy8
 
 namespace RAMCloud {

@@ -200,6 +200,23 @@ int ramcrc_segment_walk_device(ramcrc_ctx* ctx, const void* d_base, uint64_t seg
                                ramcrc_seg_entry* d_entries, uint64_t entries_cap,
                                uint64_t* d_n_entries, void* stream);
 
+/* Certificates of rebuilt segments (second half): a
+ * backup seals every recovery segment it rebuilt with
+ * Segment::getAppendedLength (src/Segment.cc:672-684, called at
+ * src/BackupMasterRecovery.cc:367-368 for the segments
+ * RecoverySegmentBuilder::build appended, src/RecoverySegmentBuilder.cc:195).
+ * For n_seg segments at d_base + i*seg_stride (seg_capacity bytes each, the
+ * walk's geometry rules) whose entries were appended from offset 0 up to
+ * d_heads[i] (Segment::head), writes d_certs[i] = {head, checksum}: the
+ * running Crc32C over every entry's header byte and length bytes, then over
+ * the 4 head bytes, finalized -- the metadata the walk covers.  d_flags
+ * (nullable) receives RAMCRC_SEG_OK when the entries end exactly at the head,
+ * else the walk's RAMCRC_SEG_PAST_CAPACITY / _PAST_LENGTH / _CYCLE findings
+ * (the certificate then covers the entries the walk read).  Stream-ordered. */
+int ramcrc_segments_certify_device(ramcrc_ctx* ctx, const void* d_base, uint64_t seg_stride,
+                                   uint32_t seg_capacity, uint64_t n_seg, const uint32_t* d_heads,
+                                   ramcrc_seg_cert* d_certs, uint32_t* d_flags, void* stream);
+
 /* ObjectManager::replaySegment's checksum checks for every record of a walk
  * whose segment passed the metadata check (d_status flags RAMCRC_SEG_OK;
  * records of failed segments are skipped, as RecoverySegmentBuilder::build
@@ -417,7 +434,10 @@ int ramcrc_ctx_status(ramcrc_ctx* ctx, uint32_t* status);
  * ramcrc_assemble_objects_host) check by themselves. */
 int ramcrc_ctx_check(ramcrc_ctx* ctx, void* stream);
 
-/* Diagnostics. */
+/* Diagnostics.  ramcrc_ctx_debug_bins waits for the device and copies the
+ * small-entry bin table's counts, both counter copies' cursors and
+ * histograms (5 x 161 words) to host, and the parity of the next sequence. */
+int ramcrc_ctx_debug_bins(ramcrc_ctx* ctx, uint64_t* host, uint64_t nwords, uint32_t* par_next);
 const char* ramcrc_strerror(int code);
 int ramcrc_last_hip_error(void);            /* last hipError_t seen (thread-local) */
 int ramcrc_device_count(void);

@@ -348,10 +348,23 @@ uint32_t oracle_build_object_segment(uint8_t* seg, uint32_t capacity, uint32_t v
     return n;
 }
 
-/* table: 4 uint32 per entry {segment, offset, length, header}; returns flags. */
+/* table: 4 uint32 per entry {segment, offset, length, header}; returns flags.
+ * f: the CRC update used for the metadata bytes. */
+static uint32_t check_metadata_f(const uint8_t* seg, uint64_t capacity, uint32_t cert_len,
+                                 uint32_t cert_crc, uint32_t segment, uint32_t* checksum_out,
+                                 uint32_t* n_out, uint32_t* table, uint64_t table_cap, crc_fn f);
+
 uint32_t oracle_check_metadata(const uint8_t* seg, uint64_t capacity, uint32_t cert_len,
                                uint32_t cert_crc, uint32_t segment, uint32_t* checksum_out,
                                uint32_t* n_out, uint32_t* table, uint64_t table_cap)
+{
+    return check_metadata_f(seg, capacity, cert_len, cert_crc, segment, checksum_out, n_out,
+                            table, table_cap, oracle_slicing8);
+}
+
+static uint32_t check_metadata_f(const uint8_t* seg, uint64_t capacity, uint32_t cert_len,
+                                 uint32_t cert_crc, uint32_t segment, uint32_t* checksum_out,
+                                 uint32_t* n_out, uint32_t* table, uint64_t table_cap, crc_fn f)
 {
     uint32_t offset = 0, crc = 0xFFFFFFFFu, n = 0, flags = 0;
     uint64_t steps = 0;
@@ -364,14 +377,14 @@ uint32_t oracle_check_metadata(const uint8_t* seg, uint64_t capacity, uint32_t c
             break;
         }
         uint8_t hdr = seg[offset];
-        crc = oracle_slicing8(crc, &hdr, 1);
+        crc = f(crc, &hdr, 1);
         uint32_t lb = (uint32_t)(hdr >> 6) + 1;
         uint8_t lenle[4] = {0, 0, 0, 0};
         for (uint32_t k = 0; k < lb; k++)   /* copyOut: bytes past the capacity stay 0 */
             if ((uint64_t)offset + 1 + k < capacity)
                 lenle[k] = seg[offset + 1 + k];
         uint32_t length = oracle_u32le(lenle);
-        crc = oracle_slicing8(crc, lenle, lb);
+        crc = f(crc, lenle, lb);
         uint32_t next = offset + 1 + lb + length;   /* uint32_t, as the reference */
         if ((uint64_t)next > capacity) {
             flags |= 2;
@@ -391,7 +404,7 @@ uint32_t oracle_check_metadata(const uint8_t* seg, uint64_t capacity, uint32_t c
     }
     uint8_t cl[4] = {(uint8_t)cert_len, (uint8_t)(cert_len >> 8), (uint8_t)(cert_len >> 16),
                      (uint8_t)(cert_len >> 24)};
-    uint32_t fin = ~oracle_slicing8(crc, cl, 4);
+    uint32_t fin = ~f(crc, cl, 4);
     if (!(flags & (2 | 32))) {
         if (offset > cert_len)
             flags |= 4;
@@ -445,13 +458,24 @@ uint32_t oracle_check_metadata(const uint8_t* seg, uint64_t capacity, uint32_t c
  * failed checks; shorter or unreadable records count as failures (the
  * reference would read past the entry there).  Failures are added to
  * bad_per_seg[segment] when that is non-NULL. */
+static uint64_t verify_objects_f(const uint8_t* base, uint64_t stride, const uint32_t* table,
+                                 uint64_t n, const uint8_t* seg_ok, uint32_t* crc_out,
+                                 uint32_t* bad_per_seg, crc_fn f);
+
 uint64_t oracle_verify_objects(const uint8_t* base, uint64_t stride, const uint32_t* table,
                                uint64_t n, const uint8_t* seg_ok, uint32_t* crc_out,
                                uint32_t* bad_per_seg)
 {
     /* Crc32C picks the crc32 instruction when the CPU has it
      * (src/Crc32C.h:200-206); both forms agree bit for bit */
-    const crc_fn f = oracle_have_sse42() ? oracle_sse42 : oracle_slicing8;
+    return verify_objects_f(base, stride, table, n, seg_ok, crc_out, bad_per_seg,
+                            oracle_have_sse42() ? oracle_sse42 : oracle_slicing8);
+}
+
+static uint64_t verify_objects_f(const uint8_t* base, uint64_t stride, const uint32_t* table,
+                                 uint64_t n, const uint8_t* seg_ok, uint32_t* crc_out,
+                                 uint32_t* bad_per_seg, crc_fn f)
+{
     uint64_t bad = 0;
     for (uint64_t i = 0; i < n; i++) {
         const uint32_t* r = table + 4 * i;
@@ -502,4 +526,85 @@ uint64_t oracle_verify_objects(const uint8_t* base, uint64_t stride, const uint3
         }
     }
     return bad;
+}
+
+/* ------------------------------------------------------------------------
+ * Replay baseline (bench.py): the checksum work of RecoverSegmentBenchmark's
+ * replay threads (nanobenchmarks/RecoverSegmentBenchmark.cc:90-118) -- per
+ * segment, Segment::checkMetadataIntegrity (restated walk above) and then the
+ * replaySegment checks of every record -- with whole segments round-robin
+ * over `nthreads` pinned threads.  Every CRC byte goes through `ext` (the
+ * reference's own intelCrc32C from oracle/_ref when the caller passes it),
+ * else through the SSE4.2 restatement.  certs: 2 uint32 per segment
+ * {segmentLength, checksum}.  Returns the number of segments that failed
+ * their metadata check or held a failed record. */
+struct replay_job {
+    const uint8_t* base;
+    uint64_t seg_bytes, nseg;
+    const uint32_t* certs;
+    crc_fn f;
+    int tid, nthreads, pin;
+    uint64_t failed;
+};
+
+static void* replay_worker(void* arg)
+{
+    struct replay_job* j = (struct replay_job*)arg;
+    if (j->pin) {
+        cpu_set_t all, one;
+        if (sched_getaffinity(0, sizeof(all), &all) == 0) {
+            int seen = 0;
+            for (int c = 0; c < CPU_SETSIZE; c++) {
+                if (!CPU_ISSET(c, &all))
+                    continue;
+                if (seen++ == j->tid) {
+                    CPU_ZERO(&one);
+                    CPU_SET(c, &one);
+                    pthread_setaffinity_np(pthread_self(), sizeof(one), &one);
+                    break;
+                }
+            }
+        }
+    }
+    const uint64_t cap = j->seg_bytes / 2 + 1;
+    uint32_t* table = (uint32_t*)malloc(cap * 16);
+    if (!table) {
+        j->failed = ~(uint64_t)0;
+        return NULL;
+    }
+    for (uint64_t i = (uint64_t)j->tid; i < j->nseg; i += (uint64_t)j->nthreads) {
+        const uint8_t* seg = j->base + i * j->seg_bytes;
+        uint32_t ck = 0, n = 0;
+        const uint32_t fl = check_metadata_f(seg, j->seg_bytes, j->certs[2 * i], j->certs[2 * i + 1],
+                                             0, &ck, &n, table, cap, j->f);
+        uint64_t bad = 0;
+        if (fl == 1)
+            bad = verify_objects_f(seg, j->seg_bytes, table, n, NULL, NULL, NULL, j->f);
+        j->failed += (fl != 1) || bad;
+    }
+    free(table);
+    return NULL;
+}
+
+int64_t oracle_replay_mt(const uint8_t* base, uint64_t seg_bytes, uint64_t nseg,
+                         const uint32_t* certs, int nthreads, int pin, crc_fn ext)
+{
+    if (nthreads < 1)
+        nthreads = 1;
+    if (nthreads > 256)
+        nthreads = 256;
+    pthread_t th[256];
+    struct replay_job jobs[256];
+    crc_fn f = ext ? ext : (oracle_have_sse42() ? oracle_sse42 : oracle_slicing8);
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t] = (struct replay_job){base, seg_bytes, nseg, certs, f, t, nthreads, pin, 0};
+        if (pthread_create(&th[t], NULL, replay_worker, &jobs[t]) != 0)
+            return -1;
+    }
+    uint64_t failed = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        failed += jobs[t].failed;
+    }
+    return (int64_t)failed;
 }

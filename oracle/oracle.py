@@ -70,6 +70,9 @@ def lib():
                                             ctypes.c_void_p]
         L.oracle_segments_mt.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.oracle_replay_mt.restype = ctypes.c_int64
+        L.oracle_replay_mt.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                       ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.oracle_have_sse42.restype = ctypes.c_int
         L.oracle_init()
         _lib = L
@@ -90,6 +93,10 @@ def ref():
         R.ref_segments_mt.restype = ctypes.c_int
         R.ref_segments_mt.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                       ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        R.ref_entries_mt.restype = ctypes.c_int
+        R.ref_entries_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int]
         _ref = R
     return _ref
 
@@ -154,6 +161,24 @@ def entries(base, off, length, init=None, finalize=True, impl=IMPL_SSE42):
     return out
 
 
+def ref_entries(base, off, length, init=None, finalize=True, threads=1, pin=True):
+    """The reference's own intelCrc32C (oracle/_ref) once per entry, blocks of
+    4096 entries dealt round-robin over `threads` pinned threads."""
+    base = _as_u8(base)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    length = np.ascontiguousarray(length, dtype=np.uint64)
+    n = off.size
+    if n and int((off + length).max()) > base.size:
+        raise ValueError("entry past end of base buffer")
+    out = np.empty(n, dtype=np.uint32)
+    init_a = None if init is None else np.ascontiguousarray(init, dtype=np.uint32)
+    rc = ref().ref_entries_mt(_ptr(base), _ptr(off), _ptr(length), _ptr(init_a), _ptr(out), n,
+                              threads, 1 if pin else 0, 1 if finalize else 0)
+    if rc != 0:
+        raise RuntimeError("thread start failed")
+    return out
+
+
 def segments(base, seg_bytes, nseg, threads=1, impl=IMPL_SSE42, pin=True, use_ref=False):
     """getResult() of each whole segment; threads take segments round-robin."""
     base = _as_u8(base)
@@ -211,3 +236,19 @@ def verify_objects(base, stride, table, nseg=None, seg_ok=None):
     total = lib().oracle_verify_objects(_ptr(base), stride, _ptr(table), n,
                                         None if ok is None else _ptr(ok), _ptr(crc), _ptr(bad))
     return int(total), crc[:n], bad[:nseg]
+
+
+def replay_mt(base, seg_bytes, nseg, certs, threads=1, pin=True, use_ref=False):
+    """Walk + replay checks of nseg object segments (whole segments round-robin
+    over threads); with use_ref every CRC byte goes through the reference's
+    own intelCrc32C (oracle/_ref).  Returns the number of failed segments."""
+    base = _as_u8(base)
+    certs = np.ascontiguousarray(certs, dtype=np.uint32).reshape(-1, 2)
+    if base.size < seg_bytes * nseg or certs.shape[0] < nseg:
+        raise ValueError("buffers too small")
+    ext = ctypes.cast(ref().ref_intel_crc32c, ctypes.c_void_p) if use_ref else None
+    r = lib().oracle_replay_mt(_ptr(base), seg_bytes, nseg, _ptr(certs), threads,
+                               1 if pin else 0, ext)
+    if r < 0:
+        raise RuntimeError("thread start failed")
+    return int(r)

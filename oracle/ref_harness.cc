@@ -80,4 +80,75 @@ int ref_segments_mt(const uint8_t* base, uint64_t segBytes, uint64_t nseg,
     return 0;
 }
 
+// Per-entry form: one Crc32C per log entry / object, as the reference's
+// replay and append loops call it (src/ObjectManager.cc:659-669,
+// src/Object.cc:805-819): out[i] = getResult() of an update over
+// base[off[i], off[i] + len[i]) from init[i] (0xFFFFFFFF when init is NULL),
+// or the raw state when finalize is 0.  Blocks of 4096 consecutive entries
+// are dealt round-robin to the threads, so each thread reads packed log bytes
+// sequentially.
+struct RefEntJob {
+    const uint8_t* base;
+    const uint64_t *off, *len;
+    const uint32_t* init;
+    uint32_t* out;
+    uint64_t n;
+    int tid, nthreads, pin, finalize;
+};
+
+static void pin_to(int tid)
+{
+    cpu_set_t all, one;
+    if (sched_getaffinity(0, sizeof(all), &all) != 0)
+        return;
+    int seen = 0;
+    for (int c = 0; c < CPU_SETSIZE; c++) {
+        if (!CPU_ISSET(c, &all))
+            continue;
+        if (seen++ == tid) {
+            CPU_ZERO(&one);
+            CPU_SET(c, &one);
+            pthread_setaffinity_np(pthread_self(), sizeof(one), &one);
+            return;
+        }
+    }
+}
+
+static void* refEntWorker(void* arg)
+{
+    RefEntJob* j = static_cast<RefEntJob*>(arg);
+    if (j->pin)
+        pin_to(j->tid);
+    const uint64_t kBlk = 4096;
+    for (uint64_t b = uint64_t(j->tid) * kBlk; b < j->n; b += uint64_t(j->nthreads) * kBlk) {
+        const uint64_t e = b + kBlk < j->n ? b + kBlk : j->n;
+        for (uint64_t i = b; i < e; i++) {
+            const uint32_t s = RAMCloud::intelCrc32C(j->init ? j->init[i] : 0xFFFFFFFFu,
+                                                     j->base + j->off[i], j->len[i]);
+            j->out[i] = j->finalize ? ~s : s;
+        }
+    }
+    return NULL;
+}
+
+int ref_entries_mt(const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                   const uint32_t* init, uint32_t* out, uint64_t n, int nthreads, int pin,
+                   int finalize)
+{
+    if (nthreads < 1)
+        nthreads = 1;
+    if (nthreads > 256)
+        nthreads = 256;
+    pthread_t th[256];
+    RefEntJob jobs[256];
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t] = RefEntJob{base, off, len, init, out, n, t, nthreads, pin, finalize};
+        if (pthread_create(&th[t], NULL, refEntWorker, &jobs[t]) != 0)
+            return -1;
+    }
+    for (int t = 0; t < nthreads; t++)
+        pthread_join(th[t], NULL);
+    return 0;
+}
+
 }  // extern "C"

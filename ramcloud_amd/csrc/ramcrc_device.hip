@@ -811,16 +811,15 @@ static_assert(kLdsTiny <= kLdsEntries, "k_entries' LDS holds the tiny phase's ta
 struct BinCounters {
     uint64_t cursor[kNB];     // scatter cursors, relative to start
     uint32_t hist[kNB];       // entry counts
-    uint32_t kobs[kNB];       // observed max steps (log-scale bins)
     uint32_t nlarge;          // large buffers the count pass left to k_chunks (skip_large)
-    uint32_t pad_[3];
+    uint32_t pad_;
 };
 
 struct BinTable {
     uint64_t start[kNB];      // first sorted slot of the bin (multiple of 8)
     uint64_t count[kNB];      // entries in the bin
     uint64_t items[kNB + 1];  // exclusive prefix of octets * kmax: work units
-    uint64_t kcost[kNB];      // steps charged per octet of the bin (observed max)
+    uint64_t kcost[kNB];      // steps charged per octet of the bin (its largest step count)
     BinCounters ctr[2];       // per parity; copy p ^ 1 is zeroed by sequence p's k_bin_count
 };
 
@@ -901,10 +900,20 @@ __device__ __forceinline__ uint32_t wave_bin_add(uint32_t* h, int b, bool active
     return rank;
 }
 
+// The histogram pass.  It counts entries only: an earlier form also kept the
+// largest step count of each log-scale bin with an LDS atomicMax issued,
+// lane-masked, between the wave_bin_add loops, and on gfx950 that histogram
+// came out wrong in about a quarter of the batches that had log-scale bins
+// (entries of bin 33 counted under bins 34-40, 0 of 72 batches once either
+// the atomicMax or the ds_bpermute-based wave_bin_add was removed,
+// tools/diag_plan_skip.py).  A phantom entry left a
+// bin's octet of padding slots only, whose interior loop bound Kmin - 1 then
+// wrapped: the k_entries hang of round 2.  Each log-scale bin's work estimate
+// now uses the bin's upper bound (bin_kmax).
 template <int kMode>
 __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, int skip_large)
 {
-    __shared__ uint32_t h[kNB], kmx[kNB];
+    __shared__ uint32_t h[kNB];
     __shared__ uint32_t nlarge;
     BinCounters& ctr = so.bt->ctr[so.par];
     if (blockIdx.x == 0) {
@@ -913,13 +922,12 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
         for (int t = threadIdx.x; t < kNB; t += blockDim.x) {
             nx.cursor[t] = 0;
             nx.hist[t] = 0;
-            nx.kobs[t] = 0;
         }
         if (threadIdx.x == 0)
             nx.nlarge = 0;
     }
     for (int t = threadIdx.x; t < kNB; t += blockDim.x)
-        h[t] = kmx[t] = 0;
+        h[t] = 0;
     if (threadIdx.x == 0)
         nlarge = 0;
     __syncthreads();
@@ -941,8 +949,6 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
             big += act[q] && large;
             const bool active = act[q] && !large;
             const int b = active ? bin_of(S[q], E[q]) : 0;
-            if (active && b > 32)
-                atomicMax(&kmx[b], uint32_t(entry_steps(S[q], E[q])));
             uint32_t unused;
             wave_bin_add(h, b, active, unused);
         }
@@ -952,12 +958,9 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
         }
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < kNB; t += blockDim.x) {
+    for (int t = threadIdx.x; t < kNB; t += blockDim.x)
         if (h[t])
             atomicAdd(&ctr.hist[t], h[t]);
-        if (kmx[t])
-            atomicMax(&ctr.kobs[t], kmx[t]);
-    }
     if (threadIdx.x == 0 && nlarge)
         atomicAdd(&ctr.nlarge, nlarge);
 }
@@ -985,8 +988,7 @@ __device__ __forceinline__ bool bin_layout(const Sorted& so, BinScratch& sc, boo
     if (b < 256) {
         if (b < kNB) {
             cnt = ctr.hist[b];
-            const uint32_t ko = ctr.kobs[b];
-            kc = b <= 32 ? uint64_t(b == 0 ? 1 : b) : (ko ? ko : bin_kmax(b));
+            kc = b <= 32 ? uint64_t(b == 0 ? 1 : b) : bin_kmax(b);
         }
         const uint64_t oct = (cnt + kG - 1) / kG;
         pos_c = oct * kG;
@@ -2068,6 +2070,9 @@ struct ramcrc_ctx {
     // per-object checksums of ramcrc_assemble_objects_device when d_out is NULL
     uint32_t* obj_out = nullptr;
     uint64_t obj_out_cap = 0;
+    // ramcrc_segments_certify_device scratch (uint32 words)
+    uint32_t* cert_scratch = nullptr;
+    uint64_t cert_scratch_cap = 0;
     // host staging for ramcrc_batch_host / ramcrc_stream_host
     uint8_t* h_stage = nullptr;
     uint64_t h_stage_cap = 0;
@@ -3841,6 +3846,37 @@ __global__ __launch_bounds__(256) void k_obj_stamp(BatchDesc d)
     p[3] = uint8_t(c >> 24);
 }
 
+// ramcrc_segments_certify_device: the walk's certificates are {head, 0}, so
+// the walk stops at each segment's head and its status carries the running
+// metadata checksum finished over the 4 head bytes -- exactly
+// Segment::getAppendedLength's certificate (src/Segment.cc:672-684) when the
+// entries end at the head.
+__global__ __launch_bounds__(256) void k_cert_prep(const uint32_t* heads, ramcrc_seg_cert* certs,
+                                                   uint64_t n)
+{
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n)
+        certs[i] = ramcrc_seg_cert{heads[i], 0u};
+}
+
+__global__ __launch_bounds__(256) void k_cert_emit(const ramcrc_seg_cert* tmp,
+                                                   const ramcrc_seg_status* st,
+                                                   ramcrc_seg_cert* certs, uint32_t* flags, uint64_t n)
+{
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const ramcrc_seg_status s = st[i];
+    certs[i] = ramcrc_seg_cert{tmp[i].segment_length, s.checksum};
+    if (flags) {
+        // the walk's checksum test is against the placeholder 0: only its
+        // structural findings matter here
+        const uint32_t bad = s.flags & (RAMCRC_SEG_PAST_CAPACITY | RAMCRC_SEG_PAST_LENGTH |
+                                        RAMCRC_SEG_CYCLE);
+        flags[i] = bad ? bad : RAMCRC_SEG_OK;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -3942,6 +3978,7 @@ int ramcrc_ctx_destroy(ramcrc_ctx* c)
     if (c->sidx) (void)hipFree(c->sidx);
     if (c->sinit) (void)hipFree(c->sinit);
     if (c->obj_out) (void)hipFree(c->obj_out);
+    if (c->cert_scratch) (void)hipFree(c->cert_scratch);
     if (c->walk_parts) (void)hipFree(c->walk_parts);
     if (c->walk_fallback) (void)hipFree(c->walk_fallback);
     if (c->walk_base) (void)hipFree(c->walk_base);
@@ -4064,6 +4101,29 @@ int ramcrc_ctx_scan_time(ramcrc_ctx* c, double* total_ms, uint64_t* launches)
         *total_ms = sum;
     if (launches)
         *launches = cnt;
+    return RAMCRC_OK;
+}
+
+int ramcrc_ctx_debug_bins(ramcrc_ctx* c, uint64_t* host, uint64_t nwords, uint32_t* par_next)
+{
+    if (!c || !host)
+        return RAMCRC_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    HIPCHK(hipDeviceSynchronize());
+    // count[kNB], then cursor[0][kNB], cursor[1][kNB], then hist[0], hist[1] (as uint64)
+    std::vector<uint64_t> v;
+    BinTable h;
+    HIPCHK(hipMemcpy(&h, c->bins, sizeof(BinTable), hipMemcpyDeviceToHost));
+    for (int b = 0; b < kNB; b++) v.push_back(h.count[b]);
+    for (int p = 0; p < 2; p++)
+        for (int b = 0; b < kNB; b++) v.push_back(h.ctr[p].cursor[b]);
+    for (int p = 0; p < 2; p++)
+        for (int b = 0; b < kNB; b++) v.push_back(h.ctr[p].hist[b]);
+    for (uint64_t i = 0; i < nwords && i < v.size(); i++)
+        host[i] = v[i];
+    if (par_next)
+        *par_next = c->bin_par;
     return RAMCRC_OK;
 }
 
@@ -4465,6 +4525,40 @@ int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_s
         w.only = c->walk_fallback;
     }
     hipLaunchKernelGGL(k_seg_walk, dim3(grid), dim3(kWaveSize), 0, s, w);
+    HIPCHK(hipGetLastError());
+    return RAMCRC_OK;
+}
+
+int ramcrc_segments_certify_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride,
+                                   uint32_t seg_capacity, uint64_t n_seg, const uint32_t* d_heads,
+                                   ramcrc_seg_cert* d_certs, uint32_t* d_flags, void* stream)
+{
+    if (!c)
+        return RAMCRC_EINVAL;
+    if (n_seg == 0)
+        return RAMCRC_OK;
+    if (!d_base || !d_heads || !d_certs || n_seg > 0xFFFFFFFFull)
+        return RAMCRC_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    // scratch: placeholder certificates, walk status, the walk's entry count
+    const uint64_t need = n_seg * (sizeof(ramcrc_seg_cert) + sizeof(ramcrc_seg_status)) / 4 + 2;
+    int rc = grow_device(reinterpret_cast<void**>(&c->cert_scratch), &c->cert_scratch_cap, need,
+                         sizeof(uint32_t));
+    if (rc)
+        return rc;
+    uint64_t* d_n = reinterpret_cast<uint64_t*>(c->cert_scratch);
+    ramcrc_seg_cert* tmp = reinterpret_cast<ramcrc_seg_cert*>(c->cert_scratch + 2);
+    ramcrc_seg_status* st = reinterpret_cast<ramcrc_seg_status*>(tmp + n_seg);
+    const dim3 grid(uint32_t((n_seg + 255) / 256));
+    hipLaunchKernelGGL(k_cert_prep, grid, dim3(256), 0, s, d_heads, tmp, n_seg);
+    HIPCHK(hipGetLastError());
+    rc = ramcrc_segment_walk_device(c, d_base, seg_stride, seg_capacity, n_seg, tmp, st, nullptr, 0,
+                                    d_n, stream);
+    if (rc)
+        return rc;
+    hipLaunchKernelGGL(k_cert_emit, grid, dim3(256), 0, s, tmp, st, d_certs, d_flags, n_seg);
     HIPCHK(hipGetLastError());
     return RAMCRC_OK;
 }

@@ -76,6 +76,7 @@ def lib():
         "ramcrc_stream_host": (i32, [vp, vp, u64, u64, vp, u32, i32, i32]),
         "ramcrc_segment_walk_device": (i32, [vp, vp, u64, u32, u64, vp, vp, vp, u64, vp, vp]),
         "ramcrc_verify_objects_device": (i32, [vp, vp, u64, vp, u64, vp, vp, vp, vp]),
+        "ramcrc_segments_certify_device": (i32, [vp, vp, u64, u32, u64, vp, vp, vp, vp]),
         "ramcrc_segment_fill_objects": (i32, [vp, u32, u32, u64, _c.POINTER(u32), vp]),
         "ramcrc_assemble_objects_device": (i32, [vp, vp, vp, vp, vp, u64, vp]),
         "ramcrc_assemble_objects_host": (i32, [vp, vp, vp, u64]),
@@ -104,9 +105,15 @@ def lib():
         "ramcrc_last_hip_error": (i32, []),
         "ramcrc_device_count": (i32, []),
         "ramcrc_build_info": (_c.c_char_p, []),
+        "ramcrc_ctx_debug_bins": (i32, [vp, vp, u64, _c.POINTER(u32)]),
     }
     for name, (res, args) in sig.items():
-        f = getattr(L, name)
+        try:
+            f = getattr(L, name)
+        except AttributeError:
+            if path == _build.LIB:
+                raise   # the product library must export the whole header
+            continue    # an older A/B variant (RAMCRC_LIB)
         f.restype = res
         f.argtypes = args
     _lib = L
@@ -279,6 +286,14 @@ class Context:
         (RAMCRC_OPT_WALK_PART_SHIFT)."""
         _check(lib().ramcrc_ctx_set_option(self._h, 2, int(shift)), "ramcrc_ctx_set_option")
 
+    def debug_bins(self):
+        """Diagnostics: (count[161], cursor[2][161], hist[2][161], next parity)."""
+        buf = np.zeros(5 * 161, np.uint64)
+        par = _c.c_uint32(0)
+        _check(lib().ramcrc_ctx_debug_bins(self._h, _c.c_void_p(buf.ctypes.data), buf.size,
+                                           _c.byref(par)), "ramcrc_ctx_debug_bins")
+        return buf[:161], buf[161:483].reshape(2, 161), buf[483:].reshape(2, 161), par.value
+
     def set_option(self, option, value):
         """ramcrc_ctx_set_option (OPT_* above)."""
         _check(lib().ramcrc_ctx_set_option(self._h, int(option), int(value)), "ramcrc_ctx_set_option")
@@ -324,6 +339,16 @@ class Context:
                                               _ptr(n_entries), _stream(stream))
         _check(rc, "ramcrc_segment_walk_device")
         return status
+
+    def certify(self, data, seg_stride, seg_capacity, nseg, heads, certs, flags=None, stream=None):
+        """Segment::getAppendedLength's certificate for nseg rebuilt segments
+        (ramcrc_segments_certify_device).  heads: int32 CUDA [nseg]; certs:
+        int32 CUDA [nseg, 2] out; flags: int32 CUDA [nseg] out or None."""
+        rc = lib().ramcrc_segments_certify_device(self._h, _ptr(data), seg_stride, seg_capacity, nseg,
+                                                  _ptr(heads), _ptr(certs), _ptr(flags),
+                                                  _stream(stream))
+        _check(rc, "ramcrc_segments_certify_device")
+        return certs
 
     def verify_objects(self, data, seg_stride, entries, n_entries, obj_crc, status, stream=None):
         """Object::computeChecksum + comparison for every object record of a walk."""

@@ -102,27 +102,36 @@ class RecoveryVerify:
     kernels ran on the current stream."""
 
     def __init__(self, ctx, nseg, capacity, stride=None, entries_cap=None, min_entry=None):
-        import torch
-
         self.ctx = ctx
         self.nseg = nseg
         self.capacity = capacity
         self.stride = capacity if stride is None else stride
+        # Table sizing.  Every replayed record is at least a header byte, a
+        # length byte and its type's header; the smallest is a safe version
+        # (12 B, src/Object.h:402-427), so capacity // 14 + 1 records per
+        # segment hold any segment -- but that worst case costs ~32 B of table
+        # and scan scratch per 14 segment bytes (~15 GB for 512 x 8 MiB).
+        #   entries_cap  fixed table; a walk that overflows it marks the
+        #                segment TABLE_FULL (never OK) and check() raises;
+        #   min_entry    fixed table sized for entries of at least that size;
+        #   neither      a table for 128-byte entries on average that
+        #                verify(check=True) grows (and walks again) when a walk
+        #                finds more records -- at most once per batch shape.
+        self.grow = entries_cap is None and min_entry is None
         if entries_cap is None:
-            # Every replayed record is at least a header byte, a length byte
-            # and its type's header; the smallest is a safe version (12 B,
-            # src/Object.h:402-427), so a table of capacity // 14 + 1 records
-            # per segment holds any segment of replayed records.  Callers that
-            # know their segments hold only larger entries pass entries_cap or
-            # min_entry; a walk that still overflows marks the segment
-            # TABLE_FULL (never OK) and check() raises.
-            min_entry = MIN_REPLAY_ENTRY if min_entry is None else min_entry
-            entries_cap = nseg * (capacity // min_entry + 1)
-        dev = torch.device("cuda", ctx.device)
+            per = self.GROW_START_ENTRY if self.grow else min_entry
+            entries_cap = nseg * (capacity // per + 1)
+        self._alloc(entries_cap)
+
+    GROW_START_ENTRY = 128
+
+    def _alloc(self, entries_cap):
+        import torch
+        dev = torch.device("cuda", self.ctx.device)
         self.entries = torch.zeros((entries_cap, 4), dtype=torch.int32, device=dev)
         self.n_entries = torch.zeros(1, dtype=torch.int64, device=dev)
         self.obj_crc = torch.zeros(entries_cap, dtype=torch.int32, device=dev)
-        self.status = torch.zeros((nseg, 4), dtype=torch.int32, device=dev)
+        self.status = torch.zeros((self.nseg, 4), dtype=torch.int32, device=dev)
 
     def walk(self, d_segments, d_certs, stream=None):
         self.ctx.segment_walk(d_segments, self.stride, self.capacity, self.nseg, d_certs,
@@ -137,8 +146,15 @@ class RecoveryVerify:
     def verify(self, d_segments, d_certs, stream=None, check=False):
         """Walk + per-record verify.  check=True waits for the stream and raises
         if the record table overflowed (some segment not verified) or a launch
-        was refused."""
+        was refused; a growing table (no entries_cap / min_entry given) is
+        first enlarged to the walked record count and the batch walked again."""
         self.walk(d_segments, d_certs, stream)
+        if check and self.grow:
+            self.ctx.check(stream)
+            n = int(self.n_entries.item())
+            if n > self.entries.shape[0]:
+                self._alloc(n + n // 8 + self.nseg)
+                self.walk(d_segments, d_certs, stream)
         st = self.verify_objects(d_segments, stream)
         if check:
             self.check(stream)

@@ -198,6 +198,19 @@ free_functions(const Vectors& v)
         EXPECT_EQ(v.crcByLength[i], ~RAMCloud::softwareCrc32C(0xFFFFFFFFu, in, i));
         EXPECT_EQ(v.crcByLength[i], ~slicing8(0xFFFFFFFFu, in, i));
     }
+    // the drop-in's arrays (real arrays, as the reference declares them) hold
+    // libramcrc's tables word for word
+    const uint32_t* const names[8] = {
+        Crc32CSlicingBy8::crc_tableil8_o32, Crc32CSlicingBy8::crc_tableil8_o40,
+        Crc32CSlicingBy8::crc_tableil8_o48, Crc32CSlicingBy8::crc_tableil8_o56,
+        Crc32CSlicingBy8::crc_tableil8_o64, Crc32CSlicingBy8::crc_tableil8_o72,
+        Crc32CSlicingBy8::crc_tableil8_o80, Crc32CSlicingBy8::crc_tableil8_o88};
+    const uint32_t* lib = ramcrc_slice8_tables();
+    for (int k = 0; k < 8; k++)
+        for (int b = 0; b < 256; b++)
+            EXPECT_EQ(lib[256 * k + b], names[k][b]);
+    static_assert(sizeof(Crc32CSlicingBy8::crc_tableil8_o88) == 256 * sizeof(uint32_t),
+                  "array type, as src/Crc32C.h:25-34 declares");
     std::vector<uint8_t> big(4099);
     for (size_t i = 0; i < big.size(); i++)
         big[i] = static_cast<uint8_t>((i * 40503u) >> 5);
