@@ -524,6 +524,8 @@ def run_entries(args, ranks):
     lens = workloads.entry_lengths(args.entries)
     if args.entry_size:
         lens = lens * 0 + np.uint64(args.entry_size)
+    if args.exclude_size:   # A/B: the mix without one of its sizes
+        lens = lens[lens != np.uint64(args.exclude_size)]
     offs = workloads.packed_offsets(lens)
     total = int(lens.sum())
     data = torch.empty(((total + 7) // 8) * 8, dtype=torch.uint8, device="cuda")
@@ -891,6 +893,8 @@ def parse_args(argv=None):
     ap.add_argument("--entries", type=int, default=1_000_000)
     ap.add_argument("--path", default="entries", choices=["entries", "batch"])
     ap.add_argument("--entry-size", type=int, default=0, help="fixed entry length (default: Zipf mix)")
+    ap.add_argument("--exclude-size", type=int, default=0,
+                    help="entries config: drop the entries of this size from the mix (A/B only)")
     ap.add_argument("--replay-nseg", type=int, default=512,
                     help="replay config: segments (RecoverSegmentBenchmark: 4096/8)")
     ap.add_argument("--replay-cpu-sample", type=int, default=64,

@@ -139,6 +139,12 @@ VARIANTS = {
     # k_entries ping-pong depth / waves per CU
     "pu4": ["RAMCRC_PU=4"],
     "ew8": ["RAMCRC_ENT_WAVES=8"],
+    # long-phase probes (WRONG results, A/B timing only)
+    "pfold0": ["RAMCRC_PROBE_FOLD=1"],
+    "pfoldcf": ["RAMCRC_PROBE_FOLD=2"],
+    "pmask": ["RAMCRC_PROBE_MASK=1"],
+    "pu3": ["RAMCRC_PU=3"],
+
 }
 
 

@@ -1144,9 +1144,34 @@ __device__ __forceinline__ u32x4 fix_piece(u32x4 w, uint64_t a, uint64_t S, uint
 // group's eight lanes with X^16, X^32, X^64 (a shuffle butterfly).  Every lane
 // of the group returns the entry's raw state relative to the end of its last
 // 128-byte window; the caller removes the zero padding with x^(-8 pad).
+#ifndef RAMCRC_PROBE_FOLD
+#define RAMCRC_PROBE_FOLD 0   // A/B only (WRONG results): 1 no fold lookups, 2 conflict-free fold lookups
+#endif
+#ifndef RAMCRC_PROBE_MASK
+#define RAMCRC_PROBE_MASK 0   // A/B only (WRONG results): long-phase head/tail steps unmasked
+#endif
 __device__ __forceinline__ uint32_t group_fold(const uint8_t* lds, int gl, uint32_t u0,
                                                uint32_t u1, uint32_t u2, uint32_t u3)
 {
+#if RAMCRC_PROBE_FOLD == 1
+    return u0 ^ u1 ^ u2 ^ u3 ^ uint32_t(__shfl_xor(int(u0), 1, kWaveSize));
+#elif RAMCRC_PROBE_FOLD == 2
+    auto pa = [&](uint32_t off, uint32_t v) {
+        const uint32_t* t = reinterpret_cast<const uint32_t*>(lds + off);
+        const uint32_t l = threadIdx.x & 31;
+        return t[l] ^ t[256 + l] ^ t[512 + l] ^ t[768 + l] ^ v;
+    };
+    uint32_t z = pa(kX4Off, u0) ^ u1;
+    z = pa(kX4Off, z) ^ u2;
+    z = pa(kX4Off, z) ^ u3;
+    z = pa(kX4Off, z);
+#pragma unroll
+    for (int lvl = 0; lvl < 3; lvl++) {
+        const uint32_t other = __shfl_xor(z, 1 << lvl, kWaveSize);
+        z = pa(kX4Off + (1 + lvl) * 4096, z) ^ other;
+    }
+    return z;
+#else
     uint32_t z = plain_apply(lds, kX4Off, u0) ^ u1;
     z = plain_apply(lds, kX4Off, z) ^ u2;
     z = plain_apply(lds, kX4Off, z) ^ u3;
@@ -1160,6 +1185,7 @@ __device__ __forceinline__ uint32_t group_fold(const uint8_t* lds, int gl, uint3
         z = plain_apply(lds, kX4Off + (1 + lvl) * 4096, lower_v) ^ upper_v;
     }
     return z;
+#endif
 }
 
 // Head word at distance ds = S - (word address): drop the bytes before S and
@@ -1422,15 +1448,14 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
         }
         o.S = (uint64_t(dd.y) << 32) | dd.x;
         const uint64_t E = (uint64_t(dd.w) << 32) | dd.z;
-        o.len = uint32_t(E - o.S);
-        o.A = o.S & ~uint64_t(15);
-        o.geo = (o.ix != kNoIdx && o.len >= 4) ? (o.len | (uint32_t(o.S - o.A) << 8)) : 0u;
-        if (!o.geo)
-            o.A = dummy;   // nothing to hash: the window loads read valid memory
+        const uint32_t len = uint32_t(E - o.S);   // <= 128 in bins 0-1
+        const uint64_t A = o.S & ~uint64_t(15);   // the window; not kept (registers)
+        o.geo = (o.ix != kNoIdx && len >= 4) ? (len | (uint32_t(o.S - A) << 8)) : 0u;
         // bit 12: the whole window [A, A + 128) lies in pages that hold entry
-        // bytes (or in the bin table), so its dwords can be read unclamped
-        const bool safe = !o.geo || ((o.A + 127) >> 12) == ((E - 1) >> 12);
-        o.geo |= safe ? (1u << 12) : 0u;
+        // bytes (or, with nothing to hash, in the bin table), so its dwords
+        // can be read unclamped
+        const bool safe = !o.geo || ((A + 127) >> 12) == ((E - 1) >> 12);
+        o.geo |= (safe ? (1u << 12) : 0u) | (len << 16);   // len again in bits 16-23
         return o;
     };
     // the group's eight windows: dwords gl + 8 j of each owner's window.
@@ -1444,8 +1469,10 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
         static_for8([&](auto qc) {
             constexpr int q = decltype(qc)::value;
             geo[q] = swz_from<q>(o.geo);
-            const uint64_t A = (uint64_t(swz_from<q>(uint32_t(o.A >> 32))) << 32) |
-                               swz_from<q>(uint32_t(o.A));
+            const uint64_t Sq = (uint64_t(swz_from<q>(uint32_t(o.S >> 32))) << 32) |
+                                swz_from<q>(uint32_t(o.S));
+            // nothing to hash: the window loads read valid memory (the bin table)
+            const uint64_t A = (geo[q] & 0xFFF) ? (Sq & ~uint64_t(15)) : dummy;
             const uint64_t au = A + 4 * gl;
             u32x4 v;
             if (RAMCRC_TINY_SAFE && __builtin_amdgcn_ballot_w64(!((geo[q] >> 12) & 1)) == 0) {
@@ -1530,14 +1557,15 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
         // own slot: the initial state (byte k at distance len - k), or bytewise
         if (o0.ix != kNoIdx) {
             uint32_t R;
-            if (o0.len >= 4) {
-                const uint32_t in = o0.init, n = o0.len;
+            const uint32_t n = (o0.geo >> 16) & 0xFF;   // the entry's length
+            if (n >= 4) {
+                const uint32_t in = o0.init;
                 R = mine ^ xor3(tabv(n, in & 0xFF), tabv(n - 1, (in >> 8) & 0xFF),
                                 tabv(n - 2, (in >> 16) & 0xFF)) ^
                     tabv(n - 3, in >> 24);
             } else {
                 R = o0.init;
-                for (uint32_t k = 0; k < o0.len; k++)
+                for (uint32_t k = 0; k < n; k++)
                     R = tabv(1, (R ^ *(const gu8*)(o0.S + k)) & 0xFF) ^ (R >> 8);
             }
             const uint32_t Rf = finalize ? ~R : R;
@@ -1627,240 +1655,249 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
         }
     };
 
-    for (int b = b0; b < b1; b++) {
-        const uint64_t ib = s_items[b], ie = s_items[b + 1];
-        if (ie <= lo || ib == ie)
-            continue;
-        if (ib >= hi)
-            break;
-        const uint64_t cost = s_cost[b];
-        const uint64_t oa = ((lo > ib ? lo : ib) - ib + cost - 1) / cost;
-        const uint64_t ob = ((hi < ie ? hi : ie) - ib + cost - 1) / cost;
-        const uint64_t sb = s_start[b];
-        if (oa >= ob)
-            continue;
-        if constexpr (kSmall) {
-            // Exact bins of at most kSmallK steps: the whole octet is loaded
-            // one octet ahead, so the load latency hides behind the previous
-            // octet's steps and fold instead of stalling every octet.
-            const uint32_t K = uint32_t(b);
-            struct Oct {
-                uint64_t S, E;
-                uint32_t init, ix, steps, st;
-                u32x4 w[kSmallK + 1];
-            };
-            auto load_oct = [&](uint64_t o, Oct& t) {
-                const uint64_t sl = sb + o * kG + g;
-                const u32x4 dd = so.desc[sl];
-                t.ix = so.idx[sl];
-                t.init = d.init ? so.init[sl] : 0xFFFFFFFFu;
-                t.S = (uint64_t(dd.y) << 32) | dd.x;
-                t.E = (uint64_t(dd.w) << 32) | dd.z;
-                t.steps = t.ix != kNoIdx ? uint32_t(entry_steps_line(t.S, t.E)) : 0u;   // K or K+1
-                const uint64_t A = line_base(t.S);
-                const uint64_t p0 = A + gl * 16;
-                const uint64_t safe = t.steps ? A : dummy;
-                t.st = d.vstat && t.steps ? load_u32_any(t.S - 4) : 0u;
-#pragma unroll
-                for (int k = 0; k <= kSmallK; k++) {
-                    const uint64_t a = p0 + uint64_t(k) * kStep;
-                    if (k <= int(K))
-                        t.w[k] = load16(t.steps && a < t.E ? a : safe);
+    auto run = [&]() {
+        for (int b = b0; b < b1; b++) {
+            const uint64_t ib = s_items[b], ie = s_items[b + 1];
+            if (ie <= lo || ib == ie)
+                continue;
+            if (ib >= hi)
+                break;
+            const uint64_t cost = s_cost[b];
+            const uint64_t oa = ((lo > ib ? lo : ib) - ib + cost - 1) / cost;
+            const uint64_t ob = ((hi < ie ? hi : ie) - ib + cost - 1) / cost;
+            const uint64_t sb = s_start[b];
+            if (oa >= ob)
+                continue;
+            if constexpr (kSmall) {
+                // Exact bins of at most kSmallK steps: the whole octet is loaded
+                // one octet ahead, so the load latency hides behind the previous
+                // octet's steps and fold instead of stalling every octet.
+                const uint32_t K = uint32_t(b);
+                struct Oct {
+                    uint64_t S, E;
+                    uint32_t init, ix, steps, st;
+                    u32x4 w[kSmallK + 1];
+                };
+                auto load_oct = [&](uint64_t o, Oct& t) {
+                    const uint64_t sl = sb + o * kG + g;
+                    const u32x4 dd = so.desc[sl];
+                    t.ix = so.idx[sl];
+                    t.init = d.init ? so.init[sl] : 0xFFFFFFFFu;
+                    t.S = (uint64_t(dd.y) << 32) | dd.x;
+                    t.E = (uint64_t(dd.w) << 32) | dd.z;
+                    t.steps = t.ix != kNoIdx ? uint32_t(entry_steps_line(t.S, t.E)) : 0u;   // K or K+1
+                    const uint64_t A = line_base(t.S);
+                    const uint64_t p0 = A + gl * 16;
+                    const uint64_t safe = t.steps ? A : dummy;
+                    t.st = d.vstat && t.steps ? load_u32_any(t.S - 4) : 0u;
+    #pragma unroll
+                    for (int k = 0; k <= kSmallK; k++) {
+                        const uint64_t a = p0 + uint64_t(k) * kStep;
+                        if (k <= int(K))
+                            t.w[k] = load16(t.steps && a < t.E ? a : safe);
+                    }
+                };
+                Oct cur, nxt;
+                load_oct(oa, cur);
+                for (uint64_t o = oa; o < ob; o++) {
+                    if (o + 1 < ob)
+                        load_oct(o + 1, nxt);
+                    const uint64_t A = line_base(cur.S);
+                    const uint64_t p0 = A + gl * 16;
+                    uint32_t u0 = 0, u1 = 0, u2 = 0, u3 = 0;
+                    {
+                        const int off = int(uint32_t(cur.S - A)) - 16 * gl;
+                        u32x4 w = cur.w[0];
+                        w.x = head_word(w.x, off, cur.init);
+                        w.y = head_word(w.y, off - 4, cur.init);
+                        w.z = head_word(w.z, off - 8, cur.init);
+                        w.w = head_word(w.w, off - 12, cur.init);
+                        u0 = op.apply(lds, u0, w.x);
+                        u1 = op.apply(lds, u1, w.y);
+                        u2 = op.apply(lds, u2, w.z);
+                        u3 = op.apply(lds, u3, w.w);
+                    }
+                    const int64_t erel = int64_t(cur.E - p0);
+    #pragma unroll
+                    for (int k = 1; k <= kSmallK; k++) {
+                        if (k <= int(K)) {
+                            const int64_t de64 = erel - int64_t(k) * int64_t(kStep);
+                            const int de = int(de64 < 0 ? 0 : (de64 > 16 ? 16 : de64));
+                            u32x4 w = cur.w[k];
+                            w.x &= keep_lo(de);
+                            w.y &= keep_lo(de - 4);
+                            w.z &= keep_lo(de - 8);
+                            w.w &= keep_lo(de - 12);
+                            const bool live = uint32_t(k) < cur.steps;
+                            const uint32_t v0 = op.apply(lds, u0, w.x), v1 = op.apply(lds, u1, w.y);
+                            const uint32_t v2 = op.apply(lds, u2, w.z), v3 = op.apply(lds, u3, w.w);
+                            u0 = live ? v0 : u0;
+                            u1 = live ? v1 : u1;
+                            u2 = live ? v2 : u2;
+                            u3 = live ? v3 : u3;
+                        }
+                    }
+                    pend = true;
+                    pu0 = u0;
+                    pu1 = u1;
+                    pu2 = u2;
+                    pu3 = u3;
+                    ppad = uint32_t((A + uint64_t(cur.steps) * kStep) - cur.E);
+                    pix = cur.ix;
+                    pst = cur.st;
+                    flush();
+                    cur = nxt;
                 }
-            };
-            Oct cur, nxt;
-            load_oct(oa, cur);
+            } else {
+            u32x4 nd = so.desc[sb + oa * kG + g];
+            uint32_t nix = so.idx[sb + oa * kG + g];
+            uint32_t ninit = d.init ? so.init[sb + oa * kG + g] : 0xFFFFFFFFu;
             for (uint64_t o = oa; o < ob; o++) {
-                if (o + 1 < ob)
-                    load_oct(o + 1, nxt);
-                const uint64_t A = line_base(cur.S);
+                const u32x4 dd = nd;
+                const uint32_t ix = nix, init = ninit;
+                if (o + 1 < ob) {   // prefetch the next octet's descriptor
+                    const uint64_t ns = sb + (o + 1) * kG + g;
+                    nd = so.desc[ns];
+                    nix = so.idx[ns];
+                    if (d.init)
+                        ninit = so.init[ns];
+                }
+                const uint64_t S = (uint64_t(dd.y) << 32) | dd.x;
+                const uint64_t E = (uint64_t(dd.w) << 32) | dd.z;
+                const uint32_t steps = ix != kNoIdx ? uint32_t(entry_steps_line(S, E)) : 0u;
+                const uint64_t A = line_base(S);   // windows on 128-byte lines
                 const uint64_t p0 = A + gl * 16;
+                // longest / shortest entry of the octet (padding slots excluded)
+                uint32_t kmax32 = steps, kmin32 = steps ? steps : 0xFFFFFFFFu;
+    #pragma unroll
+                for (int s = 8; s < 64; s <<= 1) {
+                    kmax32 = max(kmax32, uint32_t(__shfl_xor(kmax32, s, kWaveSize)));
+                    kmin32 = min(kmin32, uint32_t(__shfl_xor(kmin32, s, kWaveSize)));
+                }
+                const uint32_t Koct = __builtin_amdgcn_readfirstlane(kmax32);
+                const uint32_t Kmin = __builtin_amdgcn_readfirstlane(kmin32);   // >= 2
+                if (Koct == 0)
+                    continue;   // an octet of padding slots only: none in a consistent layout
+                                // (each bin's last octet holds >= 1 entry), but Kmin - 1
+                                // would bound the interior loop at 2^32 steps
+                const uint32_t kt0 = Kmin - 1;   // first tail step (>= 1)
+                const uint64_t safe = steps ? A : dummy;
+
+                // loads: head, first two tail steps, first kPU interior steps
+                const gu32x4* pb = gptr16(steps ? p0 : dummy);
+                const uint64_t bstride = steps ? kStep / 16 : 0;
+    #if RAMCRC_ENT_NT
+                auto ldf = [&](uint64_t k) -> u32x4 { return __builtin_nontemporal_load(pb + k * bstride); };
+    #else
+                auto ldf = [&](uint64_t k) -> u32x4 { return pb[k * bstride]; };
+    #endif
+                auto ldt = [&](uint32_t k) -> u32x4 {   // tail step: lanes past E read a safe word
+                    const uint64_t a = p0 + uint64_t(k) * kStep;
+                    return load16(k < steps && a < E ? a : safe);
+                };
+                const u32x4 wh = ldf(0);
+                const u32x4 wt0 = ldt(kt0);
+                const u32x4 wt1 = ldt(kt0 + 1 < Koct ? kt0 + 1 : kt0);
+                u32x4 Abuf[kPU], Bbuf[kPU];
+    #pragma unroll
+                for (int j = 0; j < kPU; j++)
+                    Abuf[j] = ldf(1 + j < kt0 ? 1 + j : 0);
+                // the stored checksum (records mode) behind the data loads; read at
+                // the octet's end
+                const uint32_t stv = d.vstat && steps ? load_u32_any(S - 4) : 0u;
+                __builtin_amdgcn_sched_barrier(0);
+                flush();
+
                 uint32_t u0 = 0, u1 = 0, u2 = 0, u3 = 0;
-                {
-                    const int off = int(uint32_t(cur.S - A)) - 16 * gl;
-                    u32x4 w = cur.w[0];
-                    w.x = head_word(w.x, off, cur.init);
-                    w.y = head_word(w.y, off - 4, cur.init);
-                    w.z = head_word(w.z, off - 8, cur.init);
-                    w.w = head_word(w.w, off - 12, cur.init);
+                auto stepf = [&](const u32x4& w) {
                     u0 = op.apply(lds, u0, w.x);
                     u1 = op.apply(lds, u1, w.y);
                     u2 = op.apply(lds, u2, w.z);
                     u3 = op.apply(lds, u3, w.w);
+                };
+                // head: keep bytes >= S, inject init at S .. S+3
+                if (RAMCRC_PROBE_MASK) {
+                    stepf(wh);
+                } else {
+                    const int off = int(uint32_t(S - A)) - 16 * gl;   // S - p0
+                    u32x4 w = wh;
+                    w.x = head_word(w.x, off, init);
+                    w.y = head_word(w.y, off - 4, init);
+                    w.z = head_word(w.z, off - 8, init);
+                    w.w = head_word(w.w, off - 12, init);
+                    stepf(w);
                 }
-                const int64_t erel = int64_t(cur.E - p0);
-#pragma unroll
-                for (int k = 1; k <= kSmallK; k++) {
-                    if (k <= int(K)) {
-                        const int64_t de64 = erel - int64_t(k) * int64_t(kStep);
-                        const int de = int(de64 < 0 ? 0 : (de64 > 16 ? 16 : de64));
-                        u32x4 w = cur.w[k];
-                        w.x &= keep_lo(de);
-                        w.y &= keep_lo(de - 4);
-                        w.z &= keep_lo(de - 8);
-                        w.w &= keep_lo(de - 12);
-                        const bool live = uint32_t(k) < cur.steps;
-                        const uint32_t v0 = op.apply(lds, u0, w.x), v1 = op.apply(lds, u1, w.y);
-                        const uint32_t v2 = op.apply(lds, u2, w.z), v3 = op.apply(lds, u3, w.w);
-                        u0 = live ? v0 : u0;
-                        u1 = live ? v1 : u1;
-                        u2 = live ? v2 : u2;
-                        u3 = live ? v3 : u3;
+                // interior
+                uint32_t k = 1;
+                for (; k + 2 * kPU <= kt0; k += 2 * kPU) {
+    #pragma unroll
+                    for (int j = 0; j < kPU; j++)
+                        Bbuf[j] = ldf(k + kPU + j);
+                    __builtin_amdgcn_sched_barrier(0);
+    #pragma unroll
+                    for (int j = 0; j < kPU; j++)
+                        stepf(Abuf[j]);
+    #pragma unroll
+                    for (int j = 0; j < kPU; j++)
+                        Abuf[j] = ldf(k + 2 * kPU + j < kt0 ? k + 2 * kPU + j : 0);
+                    __builtin_amdgcn_sched_barrier(0);
+    #pragma unroll
+                    for (int j = 0; j < kPU; j++)
+                        stepf(Bbuf[j]);
+                }
+    #pragma unroll
+                for (int j = 0; j < kPU; j++)
+                    if (k + j < kt0)
+                        stepf(Abuf[j]);
+                if (k + kPU < kt0) {
+    #pragma unroll
+                    for (int j = 0; j < kPU; j++)
+                        Bbuf[j] = ldf(k + kPU + j < kt0 ? k + kPU + j : 0);
+    #pragma unroll
+                    for (int j = 0; j < kPU; j++)
+                        if (k + kPU + j < kt0)
+                            stepf(Bbuf[j]);
+                }
+                // tail: keep bytes < E; lanes whose entry has ended stay frozen
+                const int64_t erel = int64_t(E - p0);
+                auto stept = [&](u32x4 w, uint32_t kk) {
+                    if (RAMCRC_PROBE_MASK) {
+                        stepf(w);
+                        return;
                     }
-                }
+                    const int64_t de64 = erel - int64_t(kk) * int64_t(kStep);
+                    const int de = int(de64 < 0 ? 0 : (de64 > 16 ? 16 : de64));
+                    w.x &= keep_lo(de);
+                    w.y &= keep_lo(de - 4);
+                    w.z &= keep_lo(de - 8);
+                    w.w &= keep_lo(de - 12);
+                    const bool live = kk < steps;
+                    const uint32_t v0 = op.apply(lds, u0, w.x), v1 = op.apply(lds, u1, w.y);
+                    const uint32_t v2 = op.apply(lds, u2, w.z), v3 = op.apply(lds, u3, w.w);
+                    u0 = live ? v0 : u0;
+                    u1 = live ? v1 : u1;
+                    u2 = live ? v2 : u2;
+                    u3 = live ? v3 : u3;
+                };
+                stept(wt0, kt0);
+                if (kt0 + 1 < Koct)
+                    stept(wt1, kt0 + 1);
+                for (uint32_t kk = kt0 + 2; kk < Koct; kk++)   // ragged octets (log-scale bins)
+                    stept(ldt(kk), kk);
+
                 pend = true;
                 pu0 = u0;
                 pu1 = u1;
                 pu2 = u2;
                 pu3 = u3;
-                ppad = uint32_t((A + uint64_t(cur.steps) * kStep) - cur.E);
-                pix = cur.ix;
-                pst = cur.st;
-                flush();
-                cur = nxt;
+                ppad = uint32_t((A + uint64_t(steps) * kStep) - E);
+                pix = ix;
+                pst = stv;
             }
-        } else {
-        u32x4 nd = so.desc[sb + oa * kG + g];
-        uint32_t nix = so.idx[sb + oa * kG + g];
-        uint32_t ninit = d.init ? so.init[sb + oa * kG + g] : 0xFFFFFFFFu;
-        for (uint64_t o = oa; o < ob; o++) {
-            const u32x4 dd = nd;
-            const uint32_t ix = nix, init = ninit;
-            if (o + 1 < ob) {   // prefetch the next octet's descriptor
-                const uint64_t ns = sb + (o + 1) * kG + g;
-                nd = so.desc[ns];
-                nix = so.idx[ns];
-                if (d.init)
-                    ninit = so.init[ns];
             }
-            const uint64_t S = (uint64_t(dd.y) << 32) | dd.x;
-            const uint64_t E = (uint64_t(dd.w) << 32) | dd.z;
-            const uint32_t steps = ix != kNoIdx ? uint32_t(entry_steps_line(S, E)) : 0u;
-            const uint64_t A = line_base(S);   // windows on 128-byte lines
-            const uint64_t p0 = A + gl * 16;
-            // longest / shortest entry of the octet (padding slots excluded)
-            uint32_t kmax32 = steps, kmin32 = steps ? steps : 0xFFFFFFFFu;
-#pragma unroll
-            for (int s = 8; s < 64; s <<= 1) {
-                kmax32 = max(kmax32, uint32_t(__shfl_xor(kmax32, s, kWaveSize)));
-                kmin32 = min(kmin32, uint32_t(__shfl_xor(kmin32, s, kWaveSize)));
-            }
-            const uint32_t Koct = __builtin_amdgcn_readfirstlane(kmax32);
-            const uint32_t Kmin = __builtin_amdgcn_readfirstlane(kmin32);   // >= 2
-            if (Koct == 0)
-                continue;   // an octet of padding slots only: none in a consistent layout
-                            // (each bin's last octet holds >= 1 entry), but Kmin - 1
-                            // would bound the interior loop at 2^32 steps
-            const uint32_t kt0 = Kmin - 1;   // first tail step (>= 1)
-            const uint64_t safe = steps ? A : dummy;
-
-            // loads: head, first two tail steps, first kPU interior steps
-            const gu32x4* pb = gptr16(steps ? p0 : dummy);
-            const uint64_t bstride = steps ? kStep / 16 : 0;
-#if RAMCRC_ENT_NT
-            auto ldf = [&](uint64_t k) -> u32x4 { return __builtin_nontemporal_load(pb + k * bstride); };
-#else
-            auto ldf = [&](uint64_t k) -> u32x4 { return pb[k * bstride]; };
-#endif
-            auto ldt = [&](uint32_t k) -> u32x4 {   // tail step: lanes past E read a safe word
-                const uint64_t a = p0 + uint64_t(k) * kStep;
-                return load16(k < steps && a < E ? a : safe);
-            };
-            const u32x4 wh = ldf(0);
-            const u32x4 wt0 = ldt(kt0);
-            const u32x4 wt1 = ldt(kt0 + 1 < Koct ? kt0 + 1 : kt0);
-            u32x4 Abuf[kPU], Bbuf[kPU];
-#pragma unroll
-            for (int j = 0; j < kPU; j++)
-                Abuf[j] = ldf(1 + j < kt0 ? 1 + j : 0);
-            // the stored checksum (records mode) behind the data loads; read at
-            // the octet's end
-            const uint32_t stv = d.vstat && steps ? load_u32_any(S - 4) : 0u;
-            __builtin_amdgcn_sched_barrier(0);
-            flush();
-
-            uint32_t u0 = 0, u1 = 0, u2 = 0, u3 = 0;
-            auto stepf = [&](const u32x4& w) {
-                u0 = op.apply(lds, u0, w.x);
-                u1 = op.apply(lds, u1, w.y);
-                u2 = op.apply(lds, u2, w.z);
-                u3 = op.apply(lds, u3, w.w);
-            };
-            // head: keep bytes >= S, inject init at S .. S+3
-            {
-                const int off = int(uint32_t(S - A)) - 16 * gl;   // S - p0
-                u32x4 w = wh;
-                w.x = head_word(w.x, off, init);
-                w.y = head_word(w.y, off - 4, init);
-                w.z = head_word(w.z, off - 8, init);
-                w.w = head_word(w.w, off - 12, init);
-                stepf(w);
-            }
-            // interior
-            uint32_t k = 1;
-            for (; k + 2 * kPU <= kt0; k += 2 * kPU) {
-#pragma unroll
-                for (int j = 0; j < kPU; j++)
-                    Bbuf[j] = ldf(k + kPU + j);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int j = 0; j < kPU; j++)
-                    stepf(Abuf[j]);
-#pragma unroll
-                for (int j = 0; j < kPU; j++)
-                    Abuf[j] = ldf(k + 2 * kPU + j < kt0 ? k + 2 * kPU + j : 0);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int j = 0; j < kPU; j++)
-                    stepf(Bbuf[j]);
-            }
-#pragma unroll
-            for (int j = 0; j < kPU; j++)
-                if (k + j < kt0)
-                    stepf(Abuf[j]);
-            if (k + kPU < kt0) {
-#pragma unroll
-                for (int j = 0; j < kPU; j++)
-                    Bbuf[j] = ldf(k + kPU + j < kt0 ? k + kPU + j : 0);
-#pragma unroll
-                for (int j = 0; j < kPU; j++)
-                    if (k + kPU + j < kt0)
-                        stepf(Bbuf[j]);
-            }
-            // tail: keep bytes < E; lanes whose entry has ended stay frozen
-            const int64_t erel = int64_t(E - p0);
-            auto stept = [&](u32x4 w, uint32_t kk) {
-                const int64_t de64 = erel - int64_t(kk) * int64_t(kStep);
-                const int de = int(de64 < 0 ? 0 : (de64 > 16 ? 16 : de64));
-                w.x &= keep_lo(de);
-                w.y &= keep_lo(de - 4);
-                w.z &= keep_lo(de - 8);
-                w.w &= keep_lo(de - 12);
-                const bool live = kk < steps;
-                const uint32_t v0 = op.apply(lds, u0, w.x), v1 = op.apply(lds, u1, w.y);
-                const uint32_t v2 = op.apply(lds, u2, w.z), v3 = op.apply(lds, u3, w.w);
-                u0 = live ? v0 : u0;
-                u1 = live ? v1 : u1;
-                u2 = live ? v2 : u2;
-                u3 = live ? v3 : u3;
-            };
-            stept(wt0, kt0);
-            if (kt0 + 1 < Koct)
-                stept(wt1, kt0 + 1);
-            for (uint32_t kk = kt0 + 2; kk < Koct; kk++)   // ragged octets (log-scale bins)
-                stept(ldt(kk), kk);
-
-            pend = true;
-            pu0 = u0;
-            pu1 = u1;
-            pu2 = u2;
-            pu3 = u3;
-            ppad = uint32_t((A + uint64_t(steps) * kStep) - E);
-            pix = ix;
-            pst = stv;
         }
-        }
-    }
+    };
+    run();
     flush();
     if (nb)
         flush_batch();
