@@ -41,7 +41,7 @@ enum {
     RAMCRC_EREFUSED = -6, /* a launch found more chunks than the context's scratch holds and
                              wrote none of its outputs (see ramcrc_ctx_check) */
     RAMCRC_EINTERNAL = -7 /* a small-entry launch found its bin layout inconsistent with the
-                             entries it binned and wrote none of its outputs (an internal
+                             entries it binned; its outputs are unspecified (an internal
                              invariant; never expected -- see ramcrc_ctx_check) */
 };
 

@@ -820,6 +820,8 @@ struct BinTable {
     uint64_t count[kNB];      // entries in the bin
     uint64_t items[kNB + 1];  // exclusive prefix of octets * kmax: work units
     uint64_t kcost[kNB];      // steps charged per octet of the bin (its largest step count)
+    uint64_t direct_n;        // nonzero: every entry of this kTable batch is tiny; the tiny
+                              // phase reads the caller's table in place (nothing scattered)
     BinCounters ctr[2];       // per parity; copy p ^ 1 is zeroed by sequence p's k_bin_count
 };
 
@@ -974,20 +976,33 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
 struct BinScratch {
     uint64_t start[kNB], count[kNB];
     uint64_t wpos[4], witem[4];
+    uint32_t direct;
 };
 
 // Returns false (uniformly) when the histogram asks for more sorted slots
 // than are allocated -- possible only with a corrupted histogram; the layout
 // is then published empty, the status bit set, and nothing is scattered.
-__device__ __forceinline__ bool bin_layout(const Sorted& so, BinScratch& sc, bool publish)
+// direct_n: the table size when the batch may take the direct tiny path
+// (kTable mode), else 0.  When every entry of such a batch is tiny (bins 0-1
+// hold all of them), the layout is published empty with direct_n set and
+// nothing is scattered: k_entries' tiny phase reads the caller's (off, len,
+// init) in place, in index order.
+__device__ __forceinline__ bool bin_layout(const Sorted& so, BinScratch& sc, bool publish,
+                                          uint64_t direct_n)
 {
     BinTable* bt = so.bt;
     const BinCounters& ctr = bt->ctr[so.par];
     const int b = threadIdx.x, lane = b & 63, w = b >> 6;
+    if (threadIdx.x == 0)
+        sc.direct = direct_n && uint64_t(ctr.hist[0]) + ctr.hist[1] == direct_n;
+    __syncthreads();
+    const bool direct = sc.direct;
+    if (publish && threadIdx.x == 0)
+        bt->direct_n = direct ? direct_n : 0;
     uint64_t cnt = 0, kc = 0, ps = 0, is = 0, pos_c = 0, item_c = 0;
     if (b < 256) {
         if (b < kNB) {
-            cnt = ctr.hist[b];
+            cnt = direct ? 0 : ctr.hist[b];
             kc = b <= 32 ? uint64_t(b == 0 ? 1 : b) : bin_kmax(b);
         }
         const uint64_t oct = (cnt + kG - 1) / kG;
@@ -1057,8 +1072,10 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter(BatchDesc d, Sorted so
     __shared__ BinScratch sc;
     for (int t = threadIdx.x; t < kNB; t += blockDim.x)
         cnt[t] = 0;
-    if (!bin_layout(so, sc, blockIdx.x == 0))
+    if (!bin_layout(so, sc, blockIdx.x == 0, (kMode == kTable && RAMCRC_TINY_CF) ? d.n : 0))
         return;   // corrupted histogram: nothing is scattered, k_entries refuses
+    if (sc.direct)
+        return;   // all tiny: k_entries reads the table in place
     unsigned long long* cursor = reinterpret_cast<unsigned long long*>(so.bt->ctr[so.par].cursor);
     const uint64_t tile = uint64_t(blockDim.x) * kBinPer;
     const uint64_t n = entry_count<kMode>(d);
@@ -1420,7 +1437,8 @@ __device__ __forceinline__ bool tiny_run(const BatchDesc& d, const Sorted& so, u
 __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so, uint8_t* lds,
                                             bool bad)
 {
-    if (so.bt->start[2] == so.bt->start[0])
+    const uint64_t direct_n = so.bt->direct_n;   // all tiny: the caller's table, in place
+    if (!direct_n && so.bt->start[2] == so.bt->start[0])
         return true;   // no entry of at most one window (uniform: every wave exits)
     const int lane = threadIdx.x & (kWaveSize - 1);
     const uint32_t gl = uint32_t(lane) & 7;
@@ -1428,7 +1446,7 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
     const uint64_t wave = uint64_t(blockIdx.x) * kEntWaves +
                           __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
     const uint64_t nwaves = uint64_t(gridDim.x) * kEntWaves;
-    const uint64_t s0 = so.bt->start[0], s1 = so.bt->start[2];
+    const uint64_t s0 = direct_n ? 0 : so.bt->start[0], s1 = direct_n ? direct_n : so.bt->start[2];
     const uint64_t rounds = (s1 - s0 + 63) / 64;
     const bool finalize = d.flags & RAMCRC_FINALIZE;
     const uint64_t dummy = reinterpret_cast<uint64_t>(so.bt);
@@ -1441,10 +1459,24 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
         o.ix = kNoIdx;
         o.init = 0xFFFFFFFFu;
         if (r < rounds && sl < s1) {
-            dd = so.desc[sl];
-            o.ix = so.idx[sl];
-            if (d.init)
-                o.init = so.init[sl];
+            if (direct_n) {   // kTable: buffer sl = base + off[sl], len[sl]
+                const uint64_t S = reinterpret_cast<uint64_t>(d.base) + d.off[sl];
+                const uint64_t E = S + d.len[sl];
+                dd = u32x4{uint32_t(S), uint32_t(S >> 32), uint32_t(E), uint32_t(E >> 32)};
+                o.ix = uint32_t(sl);
+                if (d.init)
+                    o.init = d.init[sl];
+                if (E - S >= 4 && E - (S & ~uint64_t(15)) > kStep) {
+                    // not tiny after all: the histogram lied; refuse, write nothing
+                    atomicOr(so.status, kStatusSticky | kStatusBins);
+                    o.ix = kNoIdx;
+                }
+            } else {
+                dd = so.desc[sl];
+                o.ix = so.idx[sl];
+                if (d.init)
+                    o.init = so.init[sl];
+            }
         }
         o.S = (uint64_t(dd.y) << 32) | dd.x;
         const uint64_t E = (uint64_t(dd.w) << 32) | dd.z;

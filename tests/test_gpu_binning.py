@@ -146,3 +146,34 @@ def test_plan_skip_alternating(ctx, oracle_mod):
         want = oracle_mod.entries(host, offs, lens, init=init)
         assert np.array_equal(got, want), k
     ctx.check()
+
+
+@pytest.mark.parametrize("api", ["entries", "batch"])
+def test_all_tiny_batch_direct_path(ctx, ramcrc, oracle_mod, api):
+    """A batch whose every entry fits one 128-byte window (100-byte log
+    entries, 0-3 byte ones, every alignment) takes the direct tiny path:
+    nothing is scattered, the tiny phase reads the caller's table in place.
+    Bit-exact with and without initial states, raw and finalized; then a mixed
+    batch on the same context (the layout switches back)."""
+    rng = np.random.default_rng(123)
+    host = oracle_mod.splitmix_bytes(99, 1 << 20)
+    base = dev(host)
+    n = 70000
+    lens = rng.integers(0, 113, n)
+    offs = rng.integers(0, (1 << 20) - 4000, n)
+    lens[:200] = np.arange(200) % 4          # bytewise entries
+    offs[200:400] = 1024 + np.arange(200)    # every alignment
+    lens[200:400] = 128 - (offs[200:400] % 16)   # ending exactly at the window end
+    init = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+    for it in (None, init):
+        got = host_u32(run(ctx, api, base, offs, lens, it))
+        want = oracle_mod.entries(host, offs, lens, init=it)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, [(int(offs[i]) % 16, int(lens[i])) for i in bad[:8]]
+    lens2 = lens.copy()
+    lens2[::97] = 3000
+    got = host_u32(run(ctx, api, base, offs, lens2))
+    assert np.array_equal(got, oracle_mod.entries(host, offs, lens2))
+    got = host_u32(run(ctx, api, base, offs, lens))
+    assert np.array_equal(got, oracle_mod.entries(host, offs, lens))
+    ctx.check()
