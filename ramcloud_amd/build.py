@@ -145,6 +145,7 @@ VARIANTS = {
     "pmask": ["RAMCRC_PROBE_MASK=1"],
     "pu3": ["RAMCRC_PU=3"],
 
+
 }
 
 

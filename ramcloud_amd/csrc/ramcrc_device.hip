@@ -1269,15 +1269,15 @@ __device__ __forceinline__ void static_for8(F&& f)
 // Returns false (uniformly) when `bad` is set in any thread of the block: the
 // bin layout disagrees with the scatter, and no slot has been dereferenced.
 __device__ __forceinline__ bool tiny_run(const BatchDesc& d, const Sorted& so, uint8_t* lds,
-                                         bool bad)
+                                         bool bad, uint32_t blk, uint32_t nblk)
 {
     if (so.bt->start[2] == so.bt->start[0])
         return true;   // no entry of at most one window (uniform: every wave exits)
     const int lane = threadIdx.x & (kWaveSize - 1);
     const int gl = lane & 7;
-    const uint64_t wave = uint64_t(blockIdx.x) * kEntWaves +
+    const uint64_t wave = uint64_t(blk) * kEntWaves +
                           __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
-    const uint64_t nwaves = uint64_t(gridDim.x) * kEntWaves;
+    const uint64_t nwaves = uint64_t(nblk) * kEntWaves;
     const uint64_t s0 = so.bt->start[0], s1 = so.bt->start[2];
     const uint64_t rounds = (s1 - s0 + 63) / 64;
     const bool finalize = d.flags & RAMCRC_FINALIZE;
@@ -1435,7 +1435,7 @@ __device__ __forceinline__ bool tiny_run(const BatchDesc& d, const Sorted& so, u
 // no clamps are needed.  Round structure, descriptor ownership and the init
 // fold are those of tiny_run, and so is the return value.
 __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so, uint8_t* lds,
-                                            bool bad)
+                                            bool bad, uint32_t blk, uint32_t nblk)
 {
     const uint64_t direct_n = so.bt->direct_n;   // all tiny: the caller's table, in place
     if (!direct_n && so.bt->start[2] == so.bt->start[0])
@@ -1443,9 +1443,9 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
     const int lane = threadIdx.x & (kWaveSize - 1);
     const uint32_t gl = uint32_t(lane) & 7;
     const uint32_t g4 = (uint32_t(lane) >> 3) & 3;
-    const uint64_t wave = uint64_t(blockIdx.x) * kEntWaves +
+    const uint64_t wave = uint64_t(blk) * kEntWaves +
                           __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
-    const uint64_t nwaves = uint64_t(gridDim.x) * kEntWaves;
+    const uint64_t nwaves = uint64_t(nblk) * kEntWaves;
     const uint64_t s0 = direct_n ? 0 : so.bt->start[0], s1 = direct_n ? direct_n : so.bt->start[2];
     const uint64_t rounds = (s1 - s0 + 63) / 64;
     const bool finalize = d.flags & RAMCRC_FINALIZE;
@@ -1634,7 +1634,8 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
 // kSmallK+1 and up.  Two instantiations keep the register allocation of the
 // long-entry loop free of the short-entry loop's state.
 template <bool kSmall>
-__device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so, const uint8_t* lds)
+__device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so, const uint8_t* lds,
+                                            uint32_t blk, uint32_t nblk)
 {
     constexpr int b0 = kSmall ? 2 : kSmallK + 1, b1 = kSmall ? kSmallK + 1 : kNB;
     const uint64_t* s_items = reinterpret_cast<const uint64_t*>(lds + kBinOff);   // kNB + 1
@@ -1647,9 +1648,9 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
     const int lane = threadIdx.x & (kWaveSize - 1);
     const int g = lane >> 3, gl = lane & 7;
     const RepOp op(lane);
-    const uint64_t wave = uint64_t(blockIdx.x) * kEntWaves +
+    const uint64_t wave = uint64_t(blk) * kEntWaves +
                           __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
-    const uint64_t nwaves = uint64_t(gridDim.x) * kEntWaves;
+    const uint64_t nwaves = uint64_t(nblk) * kEntWaves;
     const uint64_t I0 = s_items[b0], T = s_items[b1] - I0;
     const uint64_t lo = I0 + T * wave / nwaves, hi = I0 + T * (wave + 1) / nwaves;
     const bool finalize = d.flags & RAMCRC_FINALIZE;
@@ -1954,9 +1955,9 @@ __global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc 
             atomicOr(so.status, kStatusSticky | kStatusBins);
     };
 #if RAMCRC_TINY_CF
-    const bool tiny_ok = tiny_run_cf(d, so, lds, bad);
+    const bool tiny_ok = tiny_run_cf(d, so, lds, bad, blockIdx.x, gridDim.x);
 #else
-    const bool tiny_ok = tiny_run(d, so, lds, bad);
+    const bool tiny_ok = tiny_run(d, so, lds, bad, blockIdx.x, gridDim.x);
 #endif
     if (!tiny_ok) {
         refuse();
@@ -1967,7 +1968,10 @@ __global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc 
             refuse();
         return;
     }
-    __syncthreads();   // the position table is dead: refill the LDS
+    // The position table is dead: refill the LDS.  (Splitting the grid
+    // between the two phases instead -- no barrier, no refill -- measured
+    // within 1 % on the config-3 mix and was dropped, profiles/r03/ab.)
+    __syncthreads();
     fill_replicated(lds, g_tab.stride_small);
     fill_plain(lds, kX4Off, &g_tab.comb[0].t[0][0], 4 * 1024);
     fill_plain(lds, kXinvOff, g_tab.xinv, 128);
@@ -1985,8 +1989,8 @@ __global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc 
         refuse();
         return;
     }
-    entries_run<true>(d, so, lds);
-    entries_run<false>(d, so, lds);
+    entries_run<true>(d, so, lds, blockIdx.x, gridDim.x);
+    entries_run<false>(d, so, lds, blockIdx.x, gridDim.x);
 }
 
 // ------------------------------------------------------------ k_plan
