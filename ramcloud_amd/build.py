@@ -123,6 +123,9 @@ VARIANTS = {
     "ss16": ["RAMCRC_SYNC_STAGE_KIB=16"],
     "ss8": ["RAMCRC_SYNC_STAGE_KIB=8"],
     "ss12": ["RAMCRC_SYNC_STAGE_KIB=12"],
+    "spf0": ["RAMCRC_SYNC_PF=0"],
+    "searly": ["RAMCRC_SYNC_EARLY=1"],
+    "sstrict0": ["RAMCRC_SYNC_STRICT=0"],
     "ps15": ["RAMCRC_PART_SHIFT=15"],
     "ps17": ["RAMCRC_PART_SHIFT=17"],
     "tv1": ["RAMCRC_TINY_V=1"],

@@ -2831,55 +2831,101 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v)
     return uint32_t(__builtin_amdgcn_readlane(int(v), 63));
 }
 
+// One part of the sync search.  The certificate length is loaded with the
+// stage and used a search later, so its latency is not exposed either.
+struct SyncPart {
+    uint64_t sb;       // segment base address
+    uint32_t k;        // part number in the segment
+    uint32_t B;        // first byte of the part
+    uint32_t seglen;   // certificate segment length
+};
+
+__device__ __forceinline__ SyncPart sync_part(const PWalk& w, uint64_t i)
+{
+    SyncPart P;
+    const uint64_t seg = i / w.nparts;
+    P.k = uint32_t(i - seg * w.nparts);
+    P.B = P.k << w.pshift;
+    P.seglen = w.certs[seg].segment_length;
+    P.sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
+    return P;
+}
+
+#ifndef RAMCRC_SYNC_PF
+#define RAMCRC_SYNC_PF 1   // stage loads of a wave's next part issued before this part's search
+#endif
+#ifndef RAMCRC_SYNC_STRICT
+#define RAMCRC_SYNC_STRICT 1   // candidate hops past the walk limit or of empty entries end the candidate
+#endif
+#ifndef RAMCRC_SYNC_EARLY
+#define RAMCRC_SYNC_EARLY 1   // stop at the end of the first round holding a survivor
+#endif
+
 __global__ __launch_bounds__(kSyncWaves * kWaveSize) void k_walk_sync(PWalk w)
 {
     __shared__ __attribute__((aligned(16))) uint8_t wins[kSyncWaves][kSyncStage];
     __shared__ uint16_t lists[kSyncWaves][kSyncRound];   // a round's first-hop survivors
+    constexpr uint32_t kSU = kSyncStage / 1024;
     const int lane = threadIdx.x & (kWaveSize - 1);
     const int wv = threadIdx.x / kWaveSize;
     uint8_t* win = wins[wv];
     uint16_t* list = lists[wv];
     const uint64_t nwave = uint64_t(gridDim.x) * kSyncWaves;
     const uint64_t total = w.nseg * w.nparts;
-    for (uint64_t i = uint64_t(blockIdx.x) * kSyncWaves + wv; i < total; i += nwave) {
-        const uint64_t seg = i / w.nparts;
-        const uint32_t k = uint32_t(i - seg * w.nparts);
-        if (k == 0)
-            continue;   // part 0 starts at offset 0
-        const uint32_t B = k << w.pshift;
-        const uint32_t limit = walk_limit(w, seg);
-        const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
+    // stage [B, B + kSyncStage): bytes at or past the capacity are 0.  All
+    // loads are issued before the first store (one memory latency, not one
+    // per 1 KiB); with RAMCRC_SYNC_PF the loads of the wave's next part are
+    // in flight while this part is searched.  The LDS is wave-private.
+    u32x4 v[kSU];
+    auto stage_load = [&](const SyncPart& P) {
+#pragma unroll
+        for (uint32_t u = 0; u < kSU; u++) {
+            const uint64_t a = uint64_t(P.B) + u * 1024 + uint32_t(lane) * 16;
+            v[u] = a + 16 <= w.capacity ? load16(P.sb + a) : u32x4{0u, 0u, 0u, 0u};
+        }
+    };
+    uint64_t i = uint64_t(blockIdx.x) * kSyncWaves + wv;
+    SyncPart nxt{};
+    if (RAMCRC_SYNC_PF && i < total) {
+        nxt = sync_part(w, i);
+        if (nxt.k != 0)
+            stage_load(nxt);
+    }
+    for (; i < total; i += nwave) {
+        const SyncPart P = RAMCRC_SYNC_PF ? nxt : sync_part(w, i);
+        const uint32_t B = P.B;
+        const uint64_t sb = P.sb;
+        const uint32_t limit = P.seglen < w.capacity ? P.seglen : w.capacity;   // walk_limit
         uint64_t end64 = uint64_t(B) + kSyncSpan;
         end64 = end64 < uint64_t(B) + (1ull << w.pshift) ? end64 : uint64_t(B) + (1ull << w.pshift);
         end64 = end64 < w.capacity ? end64 : w.capacity;
         const uint32_t end = uint32_t(end64 < limit ? end64 : limit);
-        if (end <= B) {
-            if (lane == 0)
+        const bool search_part = P.k != 0 && end > B;   // part 0 starts at offset 0
+        if (search_part) {
+            if (!RAMCRC_SYNC_PF)
+                stage_load(P);
+#pragma unroll
+            for (uint32_t u = 0; u < kSU; u++)
+                *reinterpret_cast<u32x4*>(win + u * 1024 + uint32_t(lane) * 16) = v[u];
+        }
+        if (RAMCRC_SYNC_PF && i + nwave < total) {
+            nxt = sync_part(w, i + nwave);
+            if (nxt.k != 0)   // (also for a part past the segment length: not known yet)
+                stage_load(nxt);
+        }
+        if (!search_part) {
+            if (P.k != 0 && lane == 0)
                 w.parts[i].start = kNoStart;
             continue;
         }
-        // stage [B, B + kSyncStage): bytes at or past the capacity are 0.
-        // All loads are issued before the first store (one memory latency,
-        // not one per 1 KiB); the LDS is wave-private.
-        {
-            u32x4 v[kSyncStage / 1024];
-#pragma unroll
-            for (uint32_t u = 0; u < kSyncStage / 1024; u++) {
-                const uint64_t a = uint64_t(B) + u * 1024 + uint32_t(lane) * 16;
-                v[u] = a + 16 <= w.capacity ? load16(sb + a) : u32x4{0u, 0u, 0u, 0u};
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < kSyncStage / 1024; u++)
-                *reinterpret_cast<u32x4*>(win + u * 1024 + uint32_t(lane) * 16) = v[u];
-        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // stores land before the reads
-        auto peek = [&](uint32_t p) -> uint64_t {   // the bytes from p (>= B)
+        auto peek_lds = [&](uint32_t p) -> uint64_t {   // the bytes from p (B <= p, p + 8 <= B + kSyncStage)
             const uint32_t o = p - B;
-            if (o + 8 <= kSyncStage) {
-                const uint32_t* w32 = reinterpret_cast<const uint32_t*>(win + (o & ~3u));
-                return ((uint64_t(w32[1]) << 32) | w32[0]) >> (8 * (o & 3));
-            }
-            return seg_peek(sb, p, w.capacity);
+            const uint32_t* w32 = reinterpret_cast<const uint32_t*>(win + (o & ~3u));
+            return ((uint64_t(w32[1]) << 32) | w32[0]) >> (8 * (o & 3));
+        };
+        auto peek = [&](uint32_t p) -> uint64_t {   // the bytes from p (>= B)
+            return p - B + 8 <= kSyncStage ? peek_lds(p) : seg_peek(sb, p, w.capacity);
         };
         // Candidates in rounds of 512 from B.  A candidate survives when its
         // chain makes kSyncHops plausible hops (or reaches the limit).  A
@@ -2890,9 +2936,14 @@ __global__ __launch_bounds__(kSyncWaves * kWaveSize) void k_walk_sync(PWalk w)
         // further ahead: the survivor whose second hop lands nearest is kept
         // (ties: the lower candidate; a junk chain that wins has met the real
         // chain within two entries, which k_walk_fix resolves in as many
-        // hops).  h lies below the first hop of every survivor (a survivor
-        // before h jumps over it, h itself hops to the next real header), so
-        // the scan stops at the nearest first hop seen.
+        // hops).  The scan ends with the first round that holds a survivor
+        // (RAMCRC_SYNC_EARLY; a junk survivor from an earlier position is then
+        // met by k_walk_fix or its part walked again), or else at the nearest
+        // first hop seen.  The guess only decides how much k_walk_fix re-walks,
+        // never a result.  Replay A/B (profiles/r03/walk): stopping early cut
+        // this kernel from 217 to 157 us on 1 KiB objects, but with the
+        // permissive hop test alone it doubled k_walk_fix (more junk guesses);
+        // with the strict test (RAMCRC_SYNC_STRICT) the step is 4.8 % faster.
         // Per round: lane l filters candidates c0 + 8 l + j (j < 8) four at a
         // time with byte-parallel (SWAR) tests on the words it holds
         // (first_hop4); the ~10 % that pass are listed in LDS and chased one
@@ -2902,17 +2953,29 @@ __global__ __launch_bounds__(kSyncWaves * kWaveSize) void k_walk_sync(PWalk w)
         // trip for any lane); otherwise beyond-window hops read global memory.
         const bool kill4 = w.capacity <= (1u << 24);   // a 4-byte length ends past it
         const bool kill3 = w.capacity <= (1u << 23);   // so does a 3-byte one >= 2^23
-        auto search = [&](bool lds_only, uint32_t to) -> uint32_t {
+        // The LDS-only instance has no global load: the waits a global peek
+        // brings would also wait for the next part's stage loads.
+        auto search = [&](auto lds_only_c, uint32_t to) -> uint32_t {
+            constexpr bool lds_only = decltype(lds_only_c)::value;
+            auto peek_any = [&](uint32_t p) -> uint64_t {
+                if constexpr (lds_only)
+                    return peek_lds(p);
+                else
+                    return peek(p);
+            };
             const uint32_t wend = B + kSyncWin;   // peeks below wend stay in LDS
             uint64_t best = ~0ull;                // (position after two hops << 32) | candidate
             uint32_t bound = 0xFFFFFFFFu;         // nearest first hop of a survivor: h lies below it
-            for (uint32_t c0 = B; c0 < to && c0 < bound; c0 += kSyncRound) {
+            for (uint32_t c0 = B; c0 < to && c0 < bound && !(RAMCRC_SYNC_EARLY && best != ~0ull);
+                 c0 += kSyncRound) {
                 const uint32_t cl = c0 + uint32_t(lane) * kSyncPer;
                 constexpr int kWords = (kSyncPer / 4 + 3) & ~1;
                 uint32_t d[kWords];   // bytes [cl, cl + kSyncPer + 8) and up to 4 more
 #pragma unroll
                 for (int u = 0; u < kWords; u += 2) {
-                    const uint64_t v = peek(cl + 4 * u);
+                    // (LDS-only: words past the window belong to candidates >= to, masked below)
+                    const uint32_t pc = cl + 4 * u;
+                    const uint64_t v = peek_any(lds_only && pc - B > kSyncStage - 8 ? B + kSyncStage - 8 : pc);
                     d[u] = uint32_t(v);
                     d[u + 1] = uint32_t(v >> 32);
                 }
@@ -2945,9 +3008,14 @@ __global__ __launch_bounds__(kSyncWaves * kWaveSize) void k_walk_sync(PWalk w)
                             if (hh > 0 && lds_only && p >= wend) {
                                 live = false;
                             } else {
-                                const uint64_t q = peek(p);
+                                const uint64_t q = peek_any(p);
                                 const Hop h = hop_of(q, p);
-                                if (plausible(q, h, w.capacity))
+                                // (guess heuristics, beyond plausible(): a real chain
+                                // neither crosses the segment length nor holds an
+                                // empty entry -- junk chains through structured
+                                // object headers do both)
+                                if (plausible(q, h, w.capacity) &&
+                                    (!RAMCRC_SYNC_STRICT || (h.next <= limit && h.len != 0)))
                                     p = uint32_t(h.next);
                                 else
                                     live = false;
@@ -2981,9 +3049,9 @@ __global__ __launch_bounds__(kSyncWaves * kWaveSize) void k_walk_sync(PWalk w)
         // entries of up to ~2 KiB: found with LDS reads alone; longer ones
         // (their chain leaves the window) by the general search
         const uint32_t lds_to = B + kSyncWin - 8 < end ? B + kSyncWin - 8 : end;
-        uint32_t guess = search(true, lds_to);
+        uint32_t guess = search(std::true_type{}, lds_to);
         if (guess == kNoStart)
-            guess = search(false, end);
+            guess = search(std::false_type{}, end);
         if (lane == 0)
             w.parts[i].start = guess;
     }
@@ -3496,6 +3564,21 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
                     } else {
 #ifdef RAMCRC_WALK_DEBUG
                         dbg_chase++;
+                        {
+                            const uint32_t g0 = uint32_t(__builtin_amdgcn_readlane(int(g.x), 0));
+                            const uint32_t g1 = uint32_t(__builtin_amdgcn_readlane(int(g.x), 1));
+                            const uint32_t g2 = uint32_t(__builtin_amdgcn_readlane(int(g.x), 2));
+                            const uint32_t l0 = uint32_t(__builtin_amdgcn_readlane(int(g.y), 0));
+                            const uint64_t q0 = seg_peek(sb, pe, w.capacity);
+                            const Hop h0 = hop_of(q0, pe);
+                            const uint64_t qg = seg_peek(sb, st, w.capacity);
+                            if (lane == 0)
+                                printf("chasedbg seg=%u part=%u B=%u pe=%u st=%u g=%u,%u,%u ghdr=%08x glen=%u "
+                                       "true_hdr=%02x true_len=%u true_next=%u qg=%016llx q0=%016llx\n",
+                                       uint32_t(seg), kj, kj << w.pshift, pe, st, g0, g1, g2, l0 & 0xFF,
+                                       l0 >> 8, uint32_t(q0 & 0xFF), h0.len, uint32_t(h0.next),
+                                       (unsigned long long)qg, (unsigned long long)q0);
+                        }
 #endif
                         // walked the whole part: its records go to the scratch and
                         // pool blocks (C copies them), or, when they do not fit, C
@@ -3734,47 +3817,75 @@ __global__ __launch_bounds__(256) void k_walk_emit(PWalk w)
     }
 }
 
-// C': the scratch records of the parts accepted without a second walk, one
-// thread per record slot (consecutive threads copy consecutive records).
+// C': the scratch records of the parts accepted without a second walk.  One
+// wave per block of kPartRec (= 64) records -- a part's first block in the
+// scratch, then the pool blocks in use -- lane j copying record j.  The copy
+// is a chain of dependent loads (block owner and records, the part's result,
+// the segment's base), so a wave takes kCopyU blocks at a time and issues
+// each level's loads for all of them together.
+static_assert(kPartRec == kWaveSize, "k_walk_copy: one lane per record of a block");
+constexpr int kCopyU = 4;
 __global__ __launch_bounds__(256) void k_walk_copy(PWalk w)
 {
-    // threads [0, parts * kPartRec): the parts' first blocks; then one per
-    // pool slot: the record it holds
-    const uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    const uint64_t nfirst = w.nseg * w.nparts * kPartRec;
-    uint64_t i;
-    uint32_t ri;
-    uint2 v;
-    if (t < nfirst) {
-        i = t / kPartRec;
-        ri = uint32_t(t - i * kPartRec);
-        v = make_uint2(0u, 0u);
-    } else {
-        const uint64_t p = t - nfirst, blk = p / kPartRec;
-        if (blk >= *w.pool_used || blk >= w.pool_cap)
-            return;
-        const uint32_t own = w.pool_owner[blk];
-        if (own == 0xFFFFFFFFu)
-            return;   // a block the fix-up wrote for a walk that met the guess
-        i = own / 16;
-        ri = (own % 16) * kPartRec + uint32_t(p - blk * kPartRec);
-        v = w.pool[p];
-    }
-    const PartRes& r = w.parts[i];
-    const uint32_t fl = r.flags;
-    if (!(fl & kPartEmit) || (fl & (kPartChase | kPartSpill)))
-        return;
-    const uint32_t n = r.count - r.pre;   // records ri = cut .. cut + n - 1
-    if (ri < r.cut || ri - r.cut >= n)
-        return;
-    const uint64_t seg = i / w.nparts;
-    if (w.fallback[seg])
-        return;
-    const uint64_t dst = w.seg_base[seg] + r.rec + r.pre + (ri - r.cut);
-    if (dst < w.cap) {
-        if (t < nfirst)
-            v = w.recs[t];
-        w.entries[dst] = u32x4{uint32_t(seg), v.x, v.y >> 8, v.y & 0xFF};
+    const uint64_t nfirst = w.nseg * w.nparts;
+    const uint64_t used = *w.pool_used;
+    const uint64_t nblk = nfirst + (used < w.pool_cap ? used : w.pool_cap);
+    const uint64_t nwave = uint64_t(gridDim.x) * (blockDim.x / kWaveSize);
+    const uint32_t lane = threadIdx.x & (kWaveSize - 1);
+    for (uint64_t b0 = (uint64_t(blockIdx.x) * (blockDim.x / kWaveSize) +
+                        __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize)) * kCopyU;
+         b0 < nblk; b0 += nwave * kCopyU) {
+        uint64_t part[kCopyU];
+        uint32_t blk[kCopyU];   // block number within the part; ~0u: nothing to copy
+        uint2 v[kCopyU];
+#pragma unroll
+        for (int u = 0; u < kCopyU; u++) {
+            const uint64_t bi = b0 + u;
+            blk[u] = ~0u;
+            part[u] = 0;
+            if (bi < nfirst) {
+                part[u] = bi;
+                blk[u] = 0;
+                v[u] = w.recs[bi * kPartRec + lane];
+            } else if (bi < nblk) {
+                const uint32_t own = w.pool_owner[bi - nfirst];
+                v[u] = w.pool[(bi - nfirst) * kPartRec + lane];
+                if (own != 0xFFFFFFFFu) {   // else a block the fix-up wrote for a walk that met the guess
+                    part[u] = own / 16;
+                    blk[u] = own % 16;
+                }
+            }
+        }
+        PartRes r[kCopyU];
+#pragma unroll
+        for (int u = 0; u < kCopyU; u++)
+            if (blk[u] != ~0u)
+                r[u] = w.parts[part[u]];
+        uint32_t fb[kCopyU];
+        uint64_t sbase[kCopyU];
+#pragma unroll
+        for (int u = 0; u < kCopyU; u++) {
+            const uint32_t fl = r[u].flags;
+            if (blk[u] != ~0u && (!(fl & kPartEmit) || (fl & (kPartChase | kPartSpill))))
+                blk[u] = ~0u;
+            if (blk[u] != ~0u) {
+                const uint64_t seg = part[u] / w.nparts;
+                fb[u] = w.fallback[seg];
+                sbase[u] = w.seg_base[seg];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kCopyU; u++) {
+            if (blk[u] == ~0u || fb[u])
+                continue;
+            const uint32_t n = r[u].count - r[u].pre;   // records ri = cut .. cut + n - 1
+            const uint32_t ri = blk[u] * kPartRec + lane;
+            if (ri < r[u].cut || ri - r[u].cut >= n)
+                continue;
+            const uint64_t dst = sbase[u] + r[u].rec + r[u].pre + (ri - r[u].cut);
+            if (dst < w.cap)
+                w.entries[dst] = u32x4{uint32_t(part[u] / w.nparts), v[u].x, v[u].y >> 8, v[u].y & 0xFF};
+        }
     }
 }
 
@@ -4592,8 +4703,10 @@ int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_s
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_walk_emit, dim3((total + 255) / 256), dim3(256), 0, s, pw);
         HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_walk_copy, dim3(((total + pool_blocks) * kPartRec + 255) / 256), dim3(256),
-                           0, s, pw);
+        uint64_t gc = (total + pool_blocks + 4 * kCopyU - 1) / (4 * kCopyU);   // kCopyU blocks per wave
+        if (gc > uint64_t(32) * c->ncu)
+            gc = uint64_t(32) * c->ncu;
+        hipLaunchKernelGGL(k_walk_copy, dim3(gc), dim3(256), 0, s, pw);
         HIPCHK(hipGetLastError());
         w.only = c->walk_fallback;
     }
