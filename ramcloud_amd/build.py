@@ -147,6 +147,14 @@ VARIANTS = {
     "pfoldcf": ["RAMCRC_PROBE_FOLD=2"],
     "pmask": ["RAMCRC_PROBE_MASK=1"],
     "pu3": ["RAMCRC_PU=3"],
+    # k_entries phase stamps (tools/stamps.py)
+    "stamps": ["RAMCRC_STAMPS=1"],
+    "stamps_sk0": ["RAMCRC_STAMPS=1", "RAMCRC_AGE_SKEW=0"],
+    "sk0": ["RAMCRC_AGE_SKEW=0"],
+    "sk30": ["RAMCRC_AGE_SKEW=30"],
+    "sk50": ["RAMCRC_AGE_SKEW=50"],
+    "sk120": ["RAMCRC_AGE_SKEW=120"],
+    "nobatch": ["RAMCRC_STEP_BATCH=0"],
 
 
 }

@@ -95,6 +95,15 @@ struct alignas(16) DeviceTables {
     uint32_t post[256 * 128 + 128];
     uint32_t xmeta[5 * 64 + 1];   // k_seg_walk: x^(8d), d = 0 .. 320 (one batch of metadata)
     uint32_t xbyte[4][256];       // x^(8 * b * 256^j): x^(8d) for any 32-bit d in 4 factors
+    // k_entries' long phase (group_fold, flush_batch, head and tail steps),
+    // laid out as in LDS from kX4Off on, so one fill copies them all:
+    struct alignas(16) LongTabs {
+        OpTable x4, x16, x32, x64;        // group_fold
+        OpTable x8;                       // X^8, the in-lane fold's second level
+        uint32_t xinv4[256];              // x^(-8 (p - 4)): unpad by p, the fold's X^4 folded in
+        uint32_t headtab[21][8];          // c = S - piece + 4 (0..20): 4 keep masks, 4 init selectors
+        uint32_t tailtab[17][4];          // bytes d (0..16) of the piece below E: 4 keep masks
+    } lt;
 };
 
 constexpr DeviceTables make_device_tables()
@@ -137,6 +146,32 @@ constexpr DeviceTables make_device_tables()
             acc = ramcrc::mulmod(acc, base);
         }
     }
+    t.lt.x4 = t.comb[0];
+    t.lt.x16 = t.comb[1];
+    t.lt.x32 = t.comb[2];
+    t.lt.x64 = t.comb[3];
+    t.lt.x8 = ramcrc::make_op(8);
+    for (int p = 0; p < 256; p++)   // x^(-8 (p - 4)) = x^(-8 p) * x^32
+        t.lt.xinv4[p] = ramcrc::mulmod(t.xinv[p], ramcrc::xpow8(4));
+    for (int c = 0; c <= 20; c++) {   // c = clamp(S - piece, -4, 16) + 4
+        const int off = c - 4;
+        for (int j = 0; j < 4; j++) {
+            uint32_t m = 0, sel = 0;
+            for (int q = 0; q < 4; q++) {
+                const int b = 4 * j + q, r = b - off;   // init byte r lands on piece byte b
+                m |= uint32_t(b >= off ? 0xFF : 0) << (8 * q);
+                // v_perm_b32(init, 0, sel): 4 + r picks init byte r, 0x0C yields 0
+                sel |= uint32_t(r >= 0 && r < 4 ? 4 + r : 0x0C) << (8 * q);
+            }
+            t.lt.headtab[c][j] = m;
+            t.lt.headtab[c][4 + j] = sel;
+        }
+    }
+    for (int d = 0; d <= 16; d++)
+        for (int j = 0; j < 4; j++) {
+            const int k = d - 4 * j < 0 ? 0 : (d - 4 * j > 4 ? 4 : d - 4 * j);
+            t.lt.tailtab[d][j] = k >= 4 ? 0xFFFFFFFFu : (1u << (8 * k)) - 1u;
+        }
     return t;
 }
 
@@ -156,13 +191,18 @@ constexpr uint32_t kRepBytes = 131072;
 constexpr uint32_t kCombOff = kRepBytes;                  // k_chunks: 7 x 4 KiB
 constexpr uint32_t kLdsChunks = kCombOff + 7 * 4096;      // 159744 B
 constexpr uint32_t kX4Off = kRepBytes;                    // k_entries: X^4,16,32,64 (16 KiB)
-constexpr uint32_t kXinvOff = kX4Off + 4 * 4096;          // k_entries: x^(-8 pad) (512 B)
-constexpr uint32_t kBinOff = kXinvOff + 512;              // k_entries: bin table (4 KiB)
-constexpr uint32_t kLdsEntries = kBinOff + 4096;          // 152064 B
+constexpr uint32_t kX8Off = kX4Off + 4 * 4096;            // k_entries: X^8 (4 KiB)
+constexpr uint32_t kXinvOff = kX8Off + 4096;              // k_entries: x^(-8 (pad - 4)) (1 KiB)
+constexpr uint32_t kHeadOff = kXinvOff + 1024;            // k_entries: head masks/selectors (672 B)
+constexpr uint32_t kTailOff = kHeadOff + 21 * 32;         // k_entries: tail masks (272 B)
+constexpr uint32_t kBinOff = kTailOff + 17 * 16;          // k_entries: bin table (4 KiB)
+constexpr uint32_t kLdsEntries = kBinOff + 4096;          // 157616 B
+static_assert(kBinOff % 16 == 0, "LDS table alignment");
+static_assert(kBinOff - kX4Off == sizeof(DeviceTables::LongTabs), "long-phase tables: LDS = g_tab.lt");
 static_assert(kLdsEntries <= 160 * 1024, "LDS budget");
 static_assert(kLdsChunks <= 160 * 1024, "LDS budget");
 #define RAMCRC_LDS_CHUNKS 159744    // reported by ramcrc_build_info
-#define RAMCRC_LDS_ENTRIES 152064
+#define RAMCRC_LDS_ENTRIES 157616
 static_assert(kLdsChunks == RAMCRC_LDS_CHUNKS && kLdsEntries == RAMCRC_LDS_ENTRIES,
               "build_info LDS sizes");
 
@@ -194,6 +234,11 @@ __device__ __forceinline__ void fill_replicated(uint8_t* lds, const OpTable& op)
         }
     }
 }
+
+// k_entries' long-phase LDS: the replicated X^128 table and g_tab.lt, every
+// global load issued before the first LDS store (one L2 round trip for the
+// whole refill instead of one per table: 5.5 -> ~2 us per launch).
+__device__ __forceinline__ void fill_long(uint8_t* lds);
 
 // words % 4 == 0; src and lds + off 16-byte aligned.
 __device__ __forceinline__ void fill_plain(uint8_t* lds, uint32_t off, const uint32_t* src,
@@ -246,6 +291,8 @@ __device__ __forceinline__ uint32_t rep_addr(uint32_t u, uint32_t lr)
     return __builtin_amdgcn_perm(u, lr, 0x0C020000u | ((4u + k) << 8));
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 struct RepOp {
     uint32_t lr0, lr1, lr2, lr3;
     __device__ explicit RepOp(int lane)
@@ -264,6 +311,14 @@ struct RepOp {
         const uint32_t d = *reinterpret_cast<const uint32_t*>(lds + rep_addr<3>(u, lr3));
         return xor3(xor3(a, b, w), c, d);
     }
+    // One Horner step of the four word accumulators, issued as k_chunks' loop
+    // runs it: the 16 table reads back to back, one wait, then the 8 XORs, so
+    // a step costs one LDS round trip.  (Under k_entries' register pressure
+    // hipcc otherwise interleaves the four lookup groups behind a wait each:
+    // four round trips per step.)  The empty asm takes every read result at
+    // once, so no XOR can be scheduled between the reads.
+    __device__ __forceinline__ void apply4(const uint8_t* lds, uint32_t& u0, uint32_t& u1,
+                                           uint32_t& u2, uint32_t& u3, const u32x4& w) const;
 };
 
 // X^d(v) through a plain (non-replicated) 4 KiB table at LDS byte offset off.
@@ -341,7 +396,6 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t v)
     return (uint64_t(hi) << 32) | lo;
 }
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // Explicit global address space: generic (flat_*) loads would also count in
 // lgkmcnt and serialise against the LDS table lookups.
 typedef const __attribute__((address_space(1))) u32x4 gu32x4;
@@ -362,6 +416,37 @@ __device__ __forceinline__ uint32_t load_u32_any(uint64_t a)
     const uint64_t b = a & ~uint64_t(3);
     const uint32_t w0 = *reinterpret_cast<g32*>(b), w1 = *reinterpret_cast<g32*>(b + 4);
     return __builtin_amdgcn_alignbyte(w1, w0, uint32_t(a) & 3);
+}
+
+#ifndef RAMCRC_STEP_BATCH
+#define RAMCRC_STEP_BATCH 1
+#endif
+__device__ __forceinline__ void RepOp::apply4(const uint8_t* lds, uint32_t& u0, uint32_t& u1,
+                                              uint32_t& u2, uint32_t& u3, const u32x4& w) const
+{
+#if RAMCRC_STEP_BATCH
+    auto rd = [&](uint32_t a) { return *reinterpret_cast<const uint32_t*>(lds + a); };
+    uint32_t a0 = rd(rep_addr<0>(u0, lr0)), a1 = rd(rep_addr<1>(u0, lr1));
+    uint32_t a2 = rd(rep_addr<2>(u0, lr2)), a3 = rd(rep_addr<3>(u0, lr3));
+    uint32_t b0 = rd(rep_addr<0>(u1, lr0)), b1 = rd(rep_addr<1>(u1, lr1));
+    uint32_t b2 = rd(rep_addr<2>(u1, lr2)), b3 = rd(rep_addr<3>(u1, lr3));
+    uint32_t c0 = rd(rep_addr<0>(u2, lr0)), c1 = rd(rep_addr<1>(u2, lr1));
+    uint32_t c2 = rd(rep_addr<2>(u2, lr2)), c3 = rd(rep_addr<3>(u2, lr3));
+    uint32_t d0 = rd(rep_addr<0>(u3, lr0)), d1 = rd(rep_addr<1>(u3, lr1));
+    uint32_t d2 = rd(rep_addr<2>(u3, lr2)), d3 = rd(rep_addr<3>(u3, lr3));
+    asm volatile(""
+                 : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3),
+                   "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3));
+    u0 = xor3(xor3(a0, a1, w.x), a2, a3);
+    u1 = xor3(xor3(b0, b1, w.y), b2, b3);
+    u2 = xor3(xor3(c0, c1, w.z), c2, c3);
+    u3 = xor3(xor3(d0, d1, w.w), d2, d3);
+#else
+    u0 = apply(lds, u0, w.x);
+    u1 = apply(lds, u1, w.y);
+    u2 = apply(lds, u2, w.z);
+    u3 = apply(lds, u3, w.w);
+#endif
 }
 
 // ------------------------------------------------------------ descriptors
@@ -787,6 +872,17 @@ constexpr int kPU = RAMCRC_PU;             // ping-pong depth (pipelined bins)
 #endif
 constexpr uint32_t kNoIdx = 0xFFFFFFFFu;   // empty slot
 constexpr uint64_t kOctetCost = 4;         // per-octet overhead in step units (work split)
+#ifndef RAMCRC_AGE_SKEW
+#define RAMCRC_AGE_SKEW 80
+#endif
+// long bins: share of a wave of age rank r (slot / 4) in 1/2000 of an equal
+// share: 2000 + skew * (3 - 2 r), i.e. +-12 % at the outer ranks for skew 80
+constexpr int kAgeSkew = RAMCRC_AGE_SKEW;
+__host__ __device__ constexpr uint64_t age_weight(uint32_t r)
+{
+    return uint64_t(2000 + kAgeSkew * (3 - 2 * int(r)));
+}
+static_assert(RAMCRC_ENT_WAVES % 4 == 0, "age ranks of four waves");
 #ifndef RAMCRC_BIN_PER
 #define RAMCRC_BIN_PER 4
 #endif
@@ -799,6 +895,43 @@ constexpr uint64_t kBinWgsPerCu = RAMCRC_BIN_WGS_PER_CU;   // binning grid cap p
 constexpr uint32_t kTinyRow0 = 3;            // tiny phase: row of distance m is m + 3
 constexpr uint32_t kLdsTiny = 132 * 1024;    // tiny phase: X^m(byte), m = -3..128
 static_assert(kLdsTiny <= kLdsEntries, "k_entries' LDS holds the tiny phase's table");
+
+__device__ __forceinline__ void fill_long(uint8_t* lds)
+{
+    constexpr uint32_t kRepItems = 4 * 256 * 8;   // as fill_replicated
+    constexpr uint32_t kPlain = sizeof(DeviceTables::LongTabs) / 16;
+    constexpr uint32_t kR = kRepItems / kEntWaves / kWaveSize;   // 8 per thread at 1024 threads
+    constexpr uint32_t kP = (kPlain + kEntWaves * kWaveSize - 1) / (kEntWaves * kWaveSize);
+    static_assert(kRepItems % (kEntWaves * kWaveSize) == 0, "rep items per thread");
+    const OpTable& op = g_tab.stride_small;
+    const uint4* src = reinterpret_cast<const uint4*>(&g_tab.lt);
+    uint32_t v[kR];
+    uint4 w[kP];
+#pragma unroll
+    for (uint32_t j = 0; j < kR; j++) {
+        const uint32_t idx = threadIdx.x + j * blockDim.x;
+        v[j] = op.t[idx >> 11][(idx >> 3) & 255];
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kP; j++) {
+        const uint32_t i = threadIdx.x + j * blockDim.x;
+        w[j] = src[i < kPlain ? i : 0];
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kR; j++) {
+        const uint32_t idx = threadIdx.x + j * blockDim.x;
+        const uint32_t k = idx >> 11, bv = (idx >> 3) & 255, q = idx & 7;
+        const uint32_t off = (k >> 1) * 65536 + bv * 256 + (k & 1) * 128 + q * 16;
+        *reinterpret_cast<uint4*>(lds + off) = make_uint4(v[j], v[j], v[j], v[j]);
+    }
+    uint4* dst = reinterpret_cast<uint4*>(lds + kX4Off);
+#pragma unroll
+    for (uint32_t j = 0; j < kP; j++) {
+        const uint32_t i = threadIdx.x + j * blockDim.x;
+        if (i < kPlain)
+            dst[i] = w[j];
+    }
+}
 
 // The counters a binning sequence (k_bin_count -> k_bin_scatter -> k_entries)
 // accumulates come in two copies selected by the sequence's parity: sequence
@@ -1189,10 +1322,12 @@ __device__ __forceinline__ uint32_t group_fold(const uint8_t* lds, int gl, uint3
     }
     return z;
 #else
-    uint32_t z = plain_apply(lds, kX4Off, u0) ^ u1;
-    z = plain_apply(lds, kX4Off, z) ^ u2;
-    z = plain_apply(lds, kX4Off, z) ^ u3;
-    z = plain_apply(lds, kX4Off, z);
+    // X^12(u0) ^ X^8(u1) ^ X^4(u2) ^ u3 as a two-level tree (the two X^4
+    // lookups are independent); the piece's final X^4 is left to the unpad
+    // constant (xinv4), so the fold is three dependent lookups deep, not four.
+    const uint32_t a = plain_apply(lds, kX4Off, u0) ^ u1;
+    const uint32_t b = plain_apply(lds, kX4Off, u2) ^ u3;
+    uint32_t z = plain_apply(lds, kX8Off, a) ^ b;
 #pragma unroll
     for (int lvl = 0; lvl < 3; lvl++) {
         const uint32_t other = __shfl_xor(z, 1 << lvl, kWaveSize);
@@ -1420,6 +1555,37 @@ __device__ __forceinline__ bool tiny_run(const BatchDesc& d, const Sorted& so, u
     return true;
 }
 
+// Probe builds only (RAMCRC_STAMPS=1, tools/stamps.py): lane 0 of every wave
+// records the 100 MHz real-time clock at k_entries' phase boundaries.
+#ifndef RAMCRC_STAMPS
+#define RAMCRC_STAMPS 0
+#endif
+#if RAMCRC_STAMPS
+constexpr int kStampWaves = 8192, kStampSlots = 8;
+__device__ unsigned long long g_stamps[kStampWaves * kStampSlots];
+#define RAMCRC_STAMP(k)                                                                       \
+    do {                                                                                      \
+        const uint32_t sw_ = blockIdx.x * kEntWaves + threadIdx.x / kWaveSize;                \
+        if ((threadIdx.x & (kWaveSize - 1)) == 0 && sw_ < uint32_t(kStampWaves))              \
+            g_stamps[sw_ * kStampSlots + (k)] = __builtin_amdgcn_s_memrealtime();             \
+    } while (0)
+#define RAMCRC_STAMP_ONCE(k, flag) \
+    do {                           \
+        if (flag) {                \
+            RAMCRC_STAMP(k);       \
+            flag = false;          \
+        }                          \
+    } while (0)
+#else
+#define RAMCRC_STAMP_ONCE(k, flag) \
+    do {                           \
+        (void)(flag);              \
+    } while (0)
+#define RAMCRC_STAMP(k) \
+    do {                \
+    } while (0)
+#endif
+
 // The tiny phase with conflict-free table lookups (RAMCRC_TINY_CF).  The
 // position table is laid out column-major, byte address 512 (255 - b) +
 // 4 (128 - m) for X^m(b) (g_tab.post), so a lookup's LDS bank is (128 - m)
@@ -1534,6 +1700,8 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
     fill_plain(lds, 0, g_tab.post, 256 * 128 + 128);
     if (__syncthreads_or(bad))
         return false;
+    RAMCRC_STAMP(5);
+    bool first_round = true;
     u32x4 wc[8];
     uint32_t gc[8], sc;
     issue(o0, wc, gc, sc);
@@ -1605,6 +1773,7 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
             if (d.vstat && Rf != sc)
                 atomicAdd(&d.vstat[d.rec[o0.ix].x].bad_objects, 1u);
         }
+        RAMCRC_STAMP_ONCE(6, first_round);
         o0 = o1;
         o1 = o2;
         sc = sn;
@@ -1652,7 +1821,6 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
                           __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
     const uint64_t nwaves = uint64_t(nblk) * kEntWaves;
     const uint64_t I0 = s_items[b0], T = s_items[b1] - I0;
-    const uint64_t lo = I0 + T * wave / nwaves, hi = I0 + T * (wave + 1) / nwaves;
     const bool finalize = d.flags & RAMCRC_FINALIZE;
     const uint64_t dummy = reinterpret_cast<uint64_t>(so.bt);   // device memory, 16 B aligned
 
@@ -1660,7 +1828,7 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
     uint32_t bY = 0, bPad = 0, bIx = kNoIdx, bSt = 0;
     int nb = 0;
     auto flush_batch = [&]() {
-        const uint32_t R = mulmod_horner(bY, xinv[bPad & 127]);
+        const uint32_t R = mulmod_horner(bY, xinv[bPad & 255]);
         if (bIx != kNoIdx) {
             const uint32_t Rf = finalize ? ~R : R;
             d.out[bIx] = Rf;
@@ -1688,7 +1856,8 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
         }
     };
 
-    auto run = [&]() {
+    // the octets whose first work unit lies in [lo, hi)
+    auto run = [&](const uint64_t lo, const uint64_t hi) {
         for (int b = b0; b < b1; b++) {
             const uint64_t ib = s_items[b], ie = s_items[b + 1];
             if (ie <= lo || ib == ie)
@@ -1745,10 +1914,7 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
                         w.y = head_word(w.y, off - 4, cur.init);
                         w.z = head_word(w.z, off - 8, cur.init);
                         w.w = head_word(w.w, off - 12, cur.init);
-                        u0 = op.apply(lds, u0, w.x);
-                        u1 = op.apply(lds, u1, w.y);
-                        u2 = op.apply(lds, u2, w.z);
-                        u3 = op.apply(lds, u3, w.w);
+                        op.apply4(lds, u0, u1, u2, u3, w);
                     }
                     const int64_t erel = int64_t(cur.E - p0);
     #pragma unroll
@@ -1762,8 +1928,8 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
                             w.z &= keep_lo(de - 8);
                             w.w &= keep_lo(de - 12);
                             const bool live = uint32_t(k) < cur.steps;
-                            const uint32_t v0 = op.apply(lds, u0, w.x), v1 = op.apply(lds, u1, w.y);
-                            const uint32_t v2 = op.apply(lds, u2, w.z), v3 = op.apply(lds, u3, w.w);
+                            uint32_t v0 = u0, v1 = u1, v2 = u2, v3 = u3;
+                            op.apply4(lds, v0, v1, v2, v3, w);
                             u0 = live ? v0 : u0;
                             u1 = live ? v1 : u1;
                             u2 = live ? v2 : u2;
@@ -1801,14 +1967,24 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
                 const uint64_t A = line_base(S);   // windows on 128-byte lines
                 const uint64_t p0 = A + gl * 16;
                 // longest / shortest entry of the octet (padding slots excluded)
-                uint32_t kmax32 = steps, kmin32 = steps ? steps : 0xFFFFFFFFu;
+                uint32_t Koct, Kmin;
+                if (b <= 32) {
+                    // exact bin b: a step count is b or b + 1 (line_base(S) lies
+                    // at most 112 bytes before the 16-byte piece of S)
+                    const bool hi = __ballot(steps == uint32_t(b) + 1) != 0;
+                    const bool lo1 = __ballot(steps == uint32_t(b)) != 0;
+                    Koct = hi ? uint32_t(b) + 1 : (lo1 ? uint32_t(b) : 0u);
+                    Kmin = lo1 ? uint32_t(b) : uint32_t(b) + 1;
+                } else {
+                    uint32_t kmax32 = steps, kmin32 = steps ? steps : 0xFFFFFFFFu;
     #pragma unroll
-                for (int s = 8; s < 64; s <<= 1) {
-                    kmax32 = max(kmax32, uint32_t(__shfl_xor(kmax32, s, kWaveSize)));
-                    kmin32 = min(kmin32, uint32_t(__shfl_xor(kmin32, s, kWaveSize)));
+                    for (int s = 8; s < 64; s <<= 1) {
+                        kmax32 = max(kmax32, uint32_t(__shfl_xor(kmax32, s, kWaveSize)));
+                        kmin32 = min(kmin32, uint32_t(__shfl_xor(kmin32, s, kWaveSize)));
+                    }
+                    Koct = __builtin_amdgcn_readfirstlane(kmax32);
+                    Kmin = __builtin_amdgcn_readfirstlane(kmin32);   // >= 2
                 }
-                const uint32_t Koct = __builtin_amdgcn_readfirstlane(kmax32);
-                const uint32_t Kmin = __builtin_amdgcn_readfirstlane(kmin32);   // >= 2
                 if (Koct == 0)
                     continue;   // an octet of padding slots only: none in a consistent layout
                                 // (each bin's last octet holds >= 1 entry), but Kmin - 1
@@ -1842,22 +2018,21 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
                 flush();
 
                 uint32_t u0 = 0, u1 = 0, u2 = 0, u3 = 0;
-                auto stepf = [&](const u32x4& w) {
-                    u0 = op.apply(lds, u0, w.x);
-                    u1 = op.apply(lds, u1, w.y);
-                    u2 = op.apply(lds, u2, w.z);
-                    u3 = op.apply(lds, u3, w.w);
-                };
-                // head: keep bytes >= S, inject init at S .. S+3
+                auto stepf = [&](const u32x4& w) { op.apply4(lds, u0, u1, u2, u3, w); };
+                // head: keep bytes >= S, inject init at S .. S+3 (masks and
+                // v_perm selectors from the LDS table of the piece's offset)
                 if (RAMCRC_PROBE_MASK) {
                     stepf(wh);
                 } else {
                     const int off = int(uint32_t(S - A)) - 16 * gl;   // S - p0
-                    u32x4 w = wh;
-                    w.x = head_word(w.x, off, init);
-                    w.y = head_word(w.y, off - 4, init);
-                    w.z = head_word(w.z, off - 8, init);
-                    w.w = head_word(w.w, off - 12, init);
+                    const int c = min(max(off, -4), 16) + 4;
+                    const u32x4* ht = reinterpret_cast<const u32x4*>(lds + kHeadOff) + 2 * c;
+                    const u32x4 m = ht[0], sl = ht[1];
+                    u32x4 w;
+                    w.x = (wh.x & m.x) ^ __builtin_amdgcn_perm(init, 0u, sl.x);
+                    w.y = (wh.y & m.y) ^ __builtin_amdgcn_perm(init, 0u, sl.y);
+                    w.z = (wh.z & m.z) ^ __builtin_amdgcn_perm(init, 0u, sl.z);
+                    w.w = (wh.w & m.w) ^ __builtin_amdgcn_perm(init, 0u, sl.w);
                     stepf(w);
                 }
                 // interior
@@ -1891,46 +2066,85 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
                         if (k + kPU + j < kt0)
                             stepf(Bbuf[j]);
                 }
-                // tail: keep bytes < E; lanes whose entry has ended stay frozen
-                const int64_t erel = int64_t(E - p0);
-                auto stept = [&](u32x4 w, uint32_t kk) {
-                    if (RAMCRC_PROBE_MASK) {
-                        stepf(w);
-                        return;
+                // tail: keep bytes < E (masks from the LDS table of the bytes
+                // left).  Every entry of the octet is live at step kt0; at
+                // kt0 + 1 the ones that have ended take one more step of zeros
+                // (no select: their padding grows by 128 bytes, < 256); the
+                // ragged steps of log-scale bins freeze ended entries.
+                const uint64_t trel64 = E - (p0 + uint64_t(kt0) * kStep);   // > 0 for live lanes
+                const int trel = int(trel64 > 1024 && int64_t(trel64) > 0 ? 1024 : int64_t(trel64));
+                const u32x4* tt = reinterpret_cast<const u32x4*>(lds + kTailOff);
+                auto stepm = [&](u32x4 w, int de) {
+                    if (!RAMCRC_PROBE_MASK) {
+                        const u32x4 m = tt[min(max(de, 0), 16)];
+                        w.x &= m.x;
+                        w.y &= m.y;
+                        w.z &= m.z;
+                        w.w &= m.w;
                     }
-                    const int64_t de64 = erel - int64_t(kk) * int64_t(kStep);
-                    const int de = int(de64 < 0 ? 0 : (de64 > 16 ? 16 : de64));
-                    w.x &= keep_lo(de);
-                    w.y &= keep_lo(de - 4);
-                    w.z &= keep_lo(de - 8);
-                    w.w &= keep_lo(de - 12);
-                    const bool live = kk < steps;
-                    const uint32_t v0 = op.apply(lds, u0, w.x), v1 = op.apply(lds, u1, w.y);
-                    const uint32_t v2 = op.apply(lds, u2, w.z), v3 = op.apply(lds, u3, w.w);
-                    u0 = live ? v0 : u0;
-                    u1 = live ? v1 : u1;
-                    u2 = live ? v2 : u2;
-                    u3 = live ? v3 : u3;
+                    stepf(w);
                 };
-                stept(wt0, kt0);
-                if (kt0 + 1 < Koct)
-                    stept(wt1, kt0 + 1);
-                for (uint32_t kk = kt0 + 2; kk < Koct; kk++)   // ragged octets (log-scale bins)
-                    stept(ldt(kk), kk);
+                stepm(wt0, trel);
+                uint32_t eff = steps;   // steps the group ran for this entry
+                if (kt0 + 1 < Koct) {
+                    stepm(wt1, trel - int(kStep));
+                    eff = steps > kt0 + 2 ? steps : kt0 + 2;
+                }
+                const int64_t erel = int64_t(E - p0);
+                for (uint32_t kk = kt0 + 2; kk < Koct; kk++) {   // ragged octets (log-scale bins)
+                    const int64_t de64 = erel - int64_t(kk) * int64_t(kStep);
+                    const uint32_t p0v = u0, p1v = u1, p2v = u2, p3v = u3;
+                    stepm(ldt(kk), int(de64 < 0 ? 0 : (de64 > 16 ? 16 : de64)));
+                    const bool live = kk < steps;
+                    u0 = live ? u0 : p0v;
+                    u1 = live ? u1 : p1v;
+                    u2 = live ? u2 : p2v;
+                    u3 = live ? u3 : p3v;
+                }
 
                 pend = true;
                 pu0 = u0;
                 pu1 = u1;
                 pu2 = u2;
                 pu3 = u3;
-                ppad = uint32_t((A + uint64_t(steps) * kStep) - E);
+                ppad = uint32_t((A + uint64_t(eff) * kStep) - E);
                 pix = ix;
                 pst = stv;
             }
             }
         }
     };
-    run();
+    // Work split.  Waves given equal shares of the long bins finish in the
+    // order they were created (phase stamps, tools/stamps.py, 1M x 4 KiB:
+    // the four oldest waves of a workgroup -- one per SIMD -- end at 564 us,
+    // the next four at 588, then 617, the youngest four at 657: each SIMD
+    // issues by age).  Each workgroup's share is therefore split among its
+    // waves by age rank (slot / 4): older waves get age_weight(rank) / 2000
+    // of an equal share.  (Taking part of the share from a counter instead -- LDS
+    // or device -- balanced the end times but cost 1.6-2.7x: every chunk
+    // restarts the descriptor -> data latency chain)
+    uint64_t lo, hi;
+    if (kSmall || kAgeSkew == 0) {
+        lo = I0 + T * wave / nwaves;
+        hi = I0 + T * (wave + 1) / nwaves;
+    } else {
+        const uint64_t P0 = I0 + T * blk / nblk, PT = I0 + T * (blk + 1) / nblk - P0;
+        const uint32_t slot = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
+        // cumulative weight of the slots before `slot` (4 slots per age rank)
+        auto cum = [](uint32_t sl) -> uint64_t {
+            uint64_t c = 0;
+#pragma unroll
+            for (uint32_t r = 0; r < kEntWaves / 4; r++) {
+                const uint32_t n = sl > 4 * r ? (sl - 4 * r < 4 ? sl - 4 * r : 4) : 0;
+                c += uint64_t(n) * age_weight(r);
+            }
+            return c;
+        };
+        const uint64_t tot = cum(kEntWaves);
+        lo = P0 + PT * cum(slot) / tot;
+        hi = P0 + PT * cum(slot + 1) / tot;
+    }
+    run(lo, hi);
     flush();
     if (nb)
         flush_batch();
@@ -1955,7 +2169,9 @@ __global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc 
             atomicOr(so.status, kStatusSticky | kStatusBins);
     };
 #if RAMCRC_TINY_CF
+    RAMCRC_STAMP(0);
     const bool tiny_ok = tiny_run_cf(d, so, lds, bad, blockIdx.x, gridDim.x);
+    RAMCRC_STAMP(1);
 #else
     const bool tiny_ok = tiny_run(d, so, lds, bad, blockIdx.x, gridDim.x);
 #endif
@@ -1972,9 +2188,7 @@ __global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc 
     // between the two phases instead -- no barrier, no refill -- measured
     // within 1 % on the config-3 mix and was dropped, profiles/r03/ab.)
     __syncthreads();
-    fill_replicated(lds, g_tab.stride_small);
-    fill_plain(lds, kX4Off, &g_tab.comb[0].t[0][0], 4 * 1024);
-    fill_plain(lds, kXinvOff, g_tab.xinv, 128);
+    fill_long(lds);
     uint64_t* s_items = reinterpret_cast<uint64_t*>(lds + kBinOff);   // kNB + 1
     uint64_t* s_start = s_items + (kNB + 1);                          // kNB
     uint32_t* s_cost = reinterpret_cast<uint32_t*>(s_start + kNB);    // kNB
@@ -1989,8 +2203,11 @@ __global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc 
         refuse();
         return;
     }
+    RAMCRC_STAMP(2);
     entries_run<true>(d, so, lds, blockIdx.x, gridDim.x);
+    RAMCRC_STAMP(3);
     entries_run<false>(d, so, lds, blockIdx.x, gridDim.x);
+    RAMCRC_STAMP(4);
 }
 
 // ------------------------------------------------------------ k_plan
@@ -4095,6 +4312,21 @@ const char* ramcrc_strerror(int code)
 #endif
 #define RAMCRC_STR2(x) #x
 #define RAMCRC_STR(x) RAMCRC_STR2(x)
+
+// Probe builds only: copies k_entries' phase stamps (RAMCRC_STAMPS) to host
+// memory; RAMCRC_EINVAL in product builds.  Not part of the C ABI header.
+int ramcrc_debug_stamps(void* out, uint64_t bytes)
+{
+#if RAMCRC_STAMPS
+    if (bytes > sizeof(g_stamps))
+        bytes = sizeof(g_stamps);
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), bytes) == hipSuccess ? RAMCRC_OK : RAMCRC_EHIP;
+#else
+    (void)out;
+    (void)bytes;
+    return RAMCRC_EINVAL;
+#endif
+}
 
 const char* ramcrc_build_info(void)
 {
