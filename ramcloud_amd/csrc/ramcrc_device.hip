@@ -1947,186 +1947,175 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
                     flush();
                     cur = nxt;
                 }
-            } else {
-            u32x4 nd = so.desc[sb + oa * kG + g];
-            uint32_t nix = so.idx[sb + oa * kG + g];
-            uint32_t ninit = d.init ? so.init[sb + oa * kG + g] : 0xFFFFFFFFu;
-            for (uint64_t o = oa; o < ob; o++) {
-                const u32x4 dd = nd;
-                const uint32_t ix = nix, init = ninit;
-                if (o + 1 < ob) {   // prefetch the next octet's descriptor
-                    const uint64_t ns = sb + (o + 1) * kG + g;
-                    nd = so.desc[ns];
-                    nix = so.idx[ns];
-                    if (d.init)
-                        ninit = so.init[ns];
-                }
-                const uint64_t S = (uint64_t(dd.y) << 32) | dd.x;
-                const uint64_t E = (uint64_t(dd.w) << 32) | dd.z;
-                const uint32_t steps = ix != kNoIdx ? uint32_t(entry_steps_line(S, E)) : 0u;
-                const uint64_t A = line_base(S);   // windows on 128-byte lines
-                const uint64_t p0 = A + gl * 16;
-                // longest / shortest entry of the octet (padding slots excluded)
-                uint32_t Koct, Kmin;
-                if (b <= 32) {
-                    // exact bin b: a step count is b or b + 1 (line_base(S) lies
-                    // at most 112 bytes before the 16-byte piece of S)
-                    const bool hi = __ballot(steps == uint32_t(b) + 1) != 0;
-                    const bool lo1 = __ballot(steps == uint32_t(b)) != 0;
-                    Koct = hi ? uint32_t(b) + 1 : (lo1 ? uint32_t(b) : 0u);
-                    Kmin = lo1 ? uint32_t(b) : uint32_t(b) + 1;
-                } else {
-                    uint32_t kmax32 = steps, kmin32 = steps ? steps : 0xFFFFFFFFu;
-    #pragma unroll
-                    for (int s = 8; s < 64; s <<= 1) {
-                        kmax32 = max(kmax32, uint32_t(__shfl_xor(kmax32, s, kWaveSize)));
-                        kmin32 = min(kmin32, uint32_t(__shfl_xor(kmin32, s, kWaveSize)));
-                    }
-                    Koct = __builtin_amdgcn_readfirstlane(kmax32);
-                    Kmin = __builtin_amdgcn_readfirstlane(kmin32);   // >= 2
-                }
-                if (Koct == 0)
-                    continue;   // an octet of padding slots only: none in a consistent layout
-                                // (each bin's last octet holds >= 1 entry), but Kmin - 1
-                                // would bound the interior loop at 2^32 steps
-                const uint32_t kt0 = Kmin - 1;   // first tail step (>= 1)
-                const uint64_t safe = steps ? A : dummy;
-
-                // loads: head, first two tail steps, first kPU interior steps
-                const gu32x4* pb = gptr16(steps ? p0 : dummy);
-                const uint64_t bstride = steps ? kStep / 16 : 0;
-    #if RAMCRC_ENT_NT
-                auto ldf = [&](uint64_t k) -> u32x4 { return __builtin_nontemporal_load(pb + k * bstride); };
-    #else
-                auto ldf = [&](uint64_t k) -> u32x4 { return pb[k * bstride]; };
-    #endif
-                auto ldt = [&](uint32_t k) -> u32x4 {   // tail step: lanes past E read a safe word
-                    const uint64_t a = p0 + uint64_t(k) * kStep;
-                    return load16(k < steps && a < E ? a : safe);
-                };
-                const u32x4 wh = ldf(0);
-                const u32x4 wt0 = ldt(kt0);
-                const u32x4 wt1 = ldt(kt0 + 1 < Koct ? kt0 + 1 : kt0);
-                u32x4 Abuf[kPU], Bbuf[kPU];
-    #pragma unroll
-                for (int j = 0; j < kPU; j++)
-                    Abuf[j] = ldf(1 + j < kt0 ? 1 + j : 0);
-                // the stored checksum (records mode) behind the data loads; read at
-                // the octet's end
-                const uint32_t stv = d.vstat && steps ? load_u32_any(S - 4) : 0u;
-                __builtin_amdgcn_sched_barrier(0);
-                flush();
-
-                uint32_t u0 = 0, u1 = 0, u2 = 0, u3 = 0;
-                auto stepf = [&](const u32x4& w) { op.apply4(lds, u0, u1, u2, u3, w); };
-                // head: keep bytes >= S, inject init at S .. S+3 (masks and
-                // v_perm selectors from the LDS table of the piece's offset)
-                if (RAMCRC_PROBE_MASK) {
-                    stepf(wh);
-                } else {
-                    const int off = int(uint32_t(S - A)) - 16 * gl;   // S - p0
-                    const int c = min(max(off, -4), 16) + 4;
-                    const u32x4* ht = reinterpret_cast<const u32x4*>(lds + kHeadOff) + 2 * c;
-                    const u32x4 m = ht[0], sl = ht[1];
-                    u32x4 w;
-                    w.x = (wh.x & m.x) ^ __builtin_amdgcn_perm(init, 0u, sl.x);
-                    w.y = (wh.y & m.y) ^ __builtin_amdgcn_perm(init, 0u, sl.y);
-                    w.z = (wh.z & m.z) ^ __builtin_amdgcn_perm(init, 0u, sl.z);
-                    w.w = (wh.w & m.w) ^ __builtin_amdgcn_perm(init, 0u, sl.w);
-                    stepf(w);
-                }
-                // interior
-                uint32_t k = 1;
-                for (; k + 2 * kPU <= kt0; k += 2 * kPU) {
-    #pragma unroll
-                    for (int j = 0; j < kPU; j++)
-                        Bbuf[j] = ldf(k + kPU + j);
-                    __builtin_amdgcn_sched_barrier(0);
-    #pragma unroll
-                    for (int j = 0; j < kPU; j++)
-                        stepf(Abuf[j]);
-    #pragma unroll
-                    for (int j = 0; j < kPU; j++)
-                        Abuf[j] = ldf(k + 2 * kPU + j < kt0 ? k + 2 * kPU + j : 0);
-                    __builtin_amdgcn_sched_barrier(0);
-    #pragma unroll
-                    for (int j = 0; j < kPU; j++)
-                        stepf(Bbuf[j]);
-                }
-    #pragma unroll
-                for (int j = 0; j < kPU; j++)
-                    if (k + j < kt0)
-                        stepf(Abuf[j]);
-                if (k + kPU < kt0) {
-    #pragma unroll
-                    for (int j = 0; j < kPU; j++)
-                        Bbuf[j] = ldf(k + kPU + j < kt0 ? k + kPU + j : 0);
-    #pragma unroll
-                    for (int j = 0; j < kPU; j++)
-                        if (k + kPU + j < kt0)
-                            stepf(Bbuf[j]);
-                }
-                // tail: keep bytes < E (masks from the LDS table of the bytes
-                // left).  Every entry of the octet is live at step kt0; at
-                // kt0 + 1 the ones that have ended take one more step of zeros
-                // (no select: their padding grows by 128 bytes, < 256); the
-                // ragged steps of log-scale bins freeze ended entries.
-                const uint64_t trel64 = E - (p0 + uint64_t(kt0) * kStep);   // > 0 for live lanes
-                const int trel = int(trel64 > 1024 && int64_t(trel64) > 0 ? 1024 : int64_t(trel64));
-                const u32x4* tt = reinterpret_cast<const u32x4*>(lds + kTailOff);
-                auto stepm = [&](u32x4 w, int de) {
-                    if (!RAMCRC_PROBE_MASK) {
-                        const u32x4 m = tt[min(max(de, 0), 16)];
-                        w.x &= m.x;
-                        w.y &= m.y;
-                        w.z &= m.z;
-                        w.w &= m.w;
-                    }
-                    stepf(w);
-                };
-                stepm(wt0, trel);
-                uint32_t eff = steps;   // steps the group ran for this entry
-                if (kt0 + 1 < Koct) {
-                    stepm(wt1, trel - int(kStep));
-                    eff = steps > kt0 + 2 ? steps : kt0 + 2;
-                }
-                const int64_t erel = int64_t(E - p0);
-                for (uint32_t kk = kt0 + 2; kk < Koct; kk++) {   // ragged octets (log-scale bins)
-                    const int64_t de64 = erel - int64_t(kk) * int64_t(kStep);
-                    const uint32_t p0v = u0, p1v = u1, p2v = u2, p3v = u3;
-                    stepm(ldt(kk), int(de64 < 0 ? 0 : (de64 > 16 ? 16 : de64)));
-                    const bool live = kk < steps;
-                    u0 = live ? u0 : p0v;
-                    u1 = live ? u1 : p1v;
-                    u2 = live ? u2 : p2v;
-                    u3 = live ? u3 : p3v;
-                }
-
-                pend = true;
-                pu0 = u0;
-                pu1 = u1;
-                pu2 = u2;
-                pu3 = u3;
-                ppad = uint32_t((A + uint64_t(eff) * kStep) - E);
-                pix = ix;
-                pst = stv;
-            }
             }
         }
     };
+    // One octet of a long bin b: 8 entries, one per lane group.
+    auto octet = [&](const u32x4 dd, const uint32_t ix, const uint32_t init, const int b) {
+            const uint64_t S = (uint64_t(dd.y) << 32) | dd.x;
+            const uint64_t E = (uint64_t(dd.w) << 32) | dd.z;
+            const uint32_t steps = ix != kNoIdx ? uint32_t(entry_steps_line(S, E)) : 0u;
+            const uint64_t A = line_base(S);   // windows on 128-byte lines
+            const uint64_t p0 = A + gl * 16;
+            // longest / shortest entry of the octet (padding slots excluded)
+            uint32_t Koct, Kmin;
+            if (b <= 32) {
+                // exact bin b: a step count is b or b + 1 (line_base(S) lies
+                // at most 112 bytes before the 16-byte piece of S)
+                const bool hi = __ballot(steps == uint32_t(b) + 1) != 0;
+                const bool lo1 = __ballot(steps == uint32_t(b)) != 0;
+                Koct = hi ? uint32_t(b) + 1 : (lo1 ? uint32_t(b) : 0u);
+                Kmin = lo1 ? uint32_t(b) : uint32_t(b) + 1;
+            } else {
+                uint32_t kmax32 = steps, kmin32 = steps ? steps : 0xFFFFFFFFu;
+#pragma unroll
+                for (int s = 8; s < 64; s <<= 1) {
+                    kmax32 = max(kmax32, uint32_t(__shfl_xor(kmax32, s, kWaveSize)));
+                    kmin32 = min(kmin32, uint32_t(__shfl_xor(kmin32, s, kWaveSize)));
+                }
+                Koct = __builtin_amdgcn_readfirstlane(kmax32);
+                Kmin = __builtin_amdgcn_readfirstlane(kmin32);   // >= 2
+            }
+            if (Koct == 0)
+                return;   // an octet of padding slots only: none in a consistent layout
+                          // (each bin's last octet holds >= 1 entry), but Kmin - 1
+                          // would bound the interior loop at 2^32 steps
+            const uint32_t kt0 = Kmin - 1;   // first tail step (>= 1)
+            const uint64_t safe = steps ? A : dummy;
+
+            // loads: head, first two tail steps, first kPU interior steps
+            const gu32x4* pb = gptr16(steps ? p0 : dummy);
+            const uint64_t bstride = steps ? kStep / 16 : 0;
+#if RAMCRC_ENT_NT
+            auto ldf = [&](uint64_t k) -> u32x4 { return __builtin_nontemporal_load(pb + k * bstride); };
+#else
+            auto ldf = [&](uint64_t k) -> u32x4 { return pb[k * bstride]; };
+#endif
+            auto ldt = [&](uint32_t k) -> u32x4 {   // tail step: lanes past E read a safe word
+                const uint64_t a = p0 + uint64_t(k) * kStep;
+                return load16(k < steps && a < E ? a : safe);
+            };
+            const u32x4 wh = ldf(0);
+            const u32x4 wt0 = ldt(kt0);
+            const u32x4 wt1 = ldt(kt0 + 1 < Koct ? kt0 + 1 : kt0);
+            u32x4 Abuf[kPU], Bbuf[kPU];
+#pragma unroll
+            for (int j = 0; j < kPU; j++)
+                Abuf[j] = ldf(1 + j < kt0 ? 1 + j : 0);
+            // the stored checksum (records mode) behind the data loads; read at
+            // the octet's end
+            const uint32_t stv = d.vstat && steps ? load_u32_any(S - 4) : 0u;
+            __builtin_amdgcn_sched_barrier(0);
+            flush();
+
+            uint32_t u0 = 0, u1 = 0, u2 = 0, u3 = 0;
+            auto stepf = [&](const u32x4& w) { op.apply4(lds, u0, u1, u2, u3, w); };
+            // head: keep bytes >= S, inject init at S .. S+3 (masks and
+            // v_perm selectors from the LDS table of the piece's offset)
+            if (RAMCRC_PROBE_MASK) {
+                stepf(wh);
+            } else {
+                const int off = int(uint32_t(S - A)) - 16 * gl;   // S - p0
+                const int c = min(max(off, -4), 16) + 4;
+                const u32x4* ht = reinterpret_cast<const u32x4*>(lds + kHeadOff) + 2 * c;
+                const u32x4 m = ht[0], sl = ht[1];
+                u32x4 w;
+                w.x = (wh.x & m.x) ^ __builtin_amdgcn_perm(init, 0u, sl.x);
+                w.y = (wh.y & m.y) ^ __builtin_amdgcn_perm(init, 0u, sl.y);
+                w.z = (wh.z & m.z) ^ __builtin_amdgcn_perm(init, 0u, sl.z);
+                w.w = (wh.w & m.w) ^ __builtin_amdgcn_perm(init, 0u, sl.w);
+                stepf(w);
+            }
+            // interior
+            uint32_t k = 1;
+            for (; k + 2 * kPU <= kt0; k += 2 * kPU) {
+#pragma unroll
+                for (int j = 0; j < kPU; j++)
+                    Bbuf[j] = ldf(k + kPU + j);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int j = 0; j < kPU; j++)
+                    stepf(Abuf[j]);
+#pragma unroll
+                for (int j = 0; j < kPU; j++)
+                    Abuf[j] = ldf(k + 2 * kPU + j < kt0 ? k + 2 * kPU + j : 0);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int j = 0; j < kPU; j++)
+                    stepf(Bbuf[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < kPU; j++)
+                if (k + j < kt0)
+                    stepf(Abuf[j]);
+            if (k + kPU < kt0) {
+#pragma unroll
+                for (int j = 0; j < kPU; j++)
+                    Bbuf[j] = ldf(k + kPU + j < kt0 ? k + kPU + j : 0);
+#pragma unroll
+                for (int j = 0; j < kPU; j++)
+                    if (k + kPU + j < kt0)
+                        stepf(Bbuf[j]);
+            }
+            // tail: keep bytes < E (masks from the LDS table of the bytes
+            // left).  Every entry of the octet is live at step kt0; at
+            // kt0 + 1 the ones that have ended take one more step of zeros
+            // (no select: their padding grows by 128 bytes, < 256); the
+            // ragged steps of log-scale bins freeze ended entries.
+            const uint64_t trel64 = E - (p0 + uint64_t(kt0) * kStep);   // > 0 for live lanes
+            const int trel = int(trel64 > 1024 && int64_t(trel64) > 0 ? 1024 : int64_t(trel64));
+            const u32x4* tt = reinterpret_cast<const u32x4*>(lds + kTailOff);
+            auto stepm = [&](u32x4 w, int de) {
+                if (!RAMCRC_PROBE_MASK) {
+                    const u32x4 m = tt[min(max(de, 0), 16)];
+                    w.x &= m.x;
+                    w.y &= m.y;
+                    w.z &= m.z;
+                    w.w &= m.w;
+                }
+                stepf(w);
+            };
+            stepm(wt0, trel);
+            uint32_t eff = steps;   // steps the group ran for this entry
+            if (kt0 + 1 < Koct) {
+                stepm(wt1, trel - int(kStep));
+                eff = steps > kt0 + 2 ? steps : kt0 + 2;
+            }
+            const int64_t erel = int64_t(E - p0);
+            for (uint32_t kk = kt0 + 2; kk < Koct; kk++) {   // ragged octets (log-scale bins)
+                const int64_t de64 = erel - int64_t(kk) * int64_t(kStep);
+                const uint32_t p0v = u0, p1v = u1, p2v = u2, p3v = u3;
+                stepm(ldt(kk), int(de64 < 0 ? 0 : (de64 > 16 ? 16 : de64)));
+                const bool live = kk < steps;
+                u0 = live ? u0 : p0v;
+                u1 = live ? u1 : p1v;
+                u2 = live ? u2 : p2v;
+                u3 = live ? u3 : p3v;
+            }
+
+            pend = true;
+            pu0 = u0;
+            pu1 = u1;
+            pu2 = u2;
+            pu3 = u3;
+            ppad = uint32_t((A + uint64_t(eff) * kStep) - E);
+            pix = ix;
+            pst = stv;
+    };
+
     // Work split.  Waves given equal shares of the long bins finish in the
     // order they were created (phase stamps, tools/stamps.py, 1M x 4 KiB:
     // the four oldest waves of a workgroup -- one per SIMD -- end at 564 us,
     // the next four at 588, then 617, the youngest four at 657: each SIMD
     // issues by age).  Each workgroup's share is therefore split among its
-    // waves by age rank (slot / 4): older waves get age_weight(rank) / 2000
-    // of an equal share.  (Taking part of the share from a counter instead -- LDS
-    // or device -- balanced the end times but cost 1.6-2.7x: every chunk
-    // restarts the descriptor -> data latency chain)
-    uint64_t lo, hi;
-    if (kSmall || kAgeSkew == 0) {
-        lo = I0 + T * wave / nwaves;
-        hi = I0 + T * (wave + 1) / nwaves;
+    // waves by age rank (slot / 4): older waves get age_weight(rank) / 2000 of
+    // an equal share.  The octets of a wave's range form one stream: the next
+    // octet's descriptor is always fetched one octet ahead, across bin
+    // boundaries too.  (Taking part of the share from a counter instead -- one
+    // LDS counter per workgroup or one device counter -- cost 1.6-2.7x, about
+    // 1-2 us per chunk; DESIGN.md section 5.4, profiles/r03/long.)
+    if constexpr (kSmall) {
+        run(I0 + T * wave / nwaves, I0 + T * (wave + 1) / nwaves);
     } else {
         const uint64_t P0 = I0 + T * blk / nblk, PT = I0 + T * (blk + 1) / nblk - P0;
         const uint32_t slot = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
@@ -2141,10 +2130,65 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
             return c;
         };
         const uint64_t tot = cum(kEntWaves);
-        lo = P0 + PT * cum(slot) / tot;
-        hi = P0 + PT * cum(slot + 1) / tot;
+        const uint64_t rlo = P0 + PT * cum(slot) / tot, rhi = P0 + PT * cum(slot + 1) / tot;
+        struct Pos {
+            int b;
+            uint64_t o, ob, sb;
+        };
+        // first octet of [rlo, rhi) in bins >= bs
+        auto seek = [&](int bs, Pos& p) -> bool {
+            for (int b = bs; b < b1; b++) {
+                const uint64_t ib = s_items[b], ie = s_items[b + 1];
+                if (ie <= rlo || ib == ie)
+                    continue;
+                if (ib >= rhi)
+                    return false;
+                const uint64_t cost = s_cost[b];
+                const uint64_t oa = ((rlo > ib ? rlo : ib) - ib + cost - 1) / cost;
+                const uint64_t ob = ((rhi < ie ? rhi : ie) - ib + cost - 1) / cost;
+                if (oa >= ob)
+                    continue;
+                p.b = b;
+                p.o = oa;
+                p.ob = ob;
+                p.sb = s_start[b];
+                return true;
+            }
+            return false;
+        };
+        // the octet after p: in its bin, else the first of the next bins
+        auto advance = [&](Pos& p) -> bool {
+            if (p.o + 1 < p.ob) {
+                p.o++;
+                return true;
+            }
+            return seek(p.b + 1, p);
+        };
+        Pos cur;
+        bool have = seek(b0, cur);
+        u32x4 nd = {0u, 0u, 0u, 0u};
+        uint32_t nix = kNoIdx, ninit = 0xFFFFFFFFu;
+        auto fetch = [&](const Pos& p) {
+            const uint64_t sl = p.sb + p.o * kG + g;
+            nd = so.desc[sl];
+            nix = so.idx[sl];
+            if (d.init)
+                ninit = so.init[sl];
+        };
+        if (have)
+            fetch(cur);
+        while (have) {
+            const u32x4 dd = nd;
+            const uint32_t ix = nix, init = ninit;
+            const int b = cur.b;
+            Pos nxt = cur;
+            have = advance(nxt);
+            if (have)   // prefetch the next octet's descriptor
+                fetch(nxt);
+            octet(dd, ix, init, b);
+            cur = nxt;
+        }
     }
-    run(lo, hi);
     flush();
     if (nb)
         flush_batch();
