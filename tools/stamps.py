@@ -82,6 +82,11 @@ def main():
     print(f"  long-done spread inside a workgroup (max - min): median {np.median(e16.max(1) - e16.min(1)):.1f}"
           f"; workgroup means: min {e16.mean(1).min():.1f} median {np.median(e16.mean(1)):.1f}"
           f" max {e16.mean(1).max():.1f}")
+    r16 = rel[: len(end) // 16 * 16, 2].reshape(-1, 16).max(1)   # workgroup's refill (tiny phase end)
+    late = r16 > np.median(r16) + 2.0
+    if late.any():
+        print(f"  workgroups whose tiny phase ended > 2 us after the median: {late.sum()}; their long-done mean "
+              f"{e16.mean(1)[late].mean():.1f} vs {e16.mean(1)[~late].mean():.1f} for the others")
     order = np.argsort(np.argsort(rel[:, 0].reshape(-1, 16), axis=1), axis=1).reshape(-1)
     print("  long-done median by start rank in workgroup:",
           " ".join(f"{np.median(end[order == x]):.1f}" for x in range(16)))
