@@ -1877,7 +1877,7 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
                 const uint32_t K = uint32_t(b);
                 struct Oct {
                     uint64_t S, E;
-                    uint32_t init, ix, steps, st;
+                    uint32_t init, ix, steps, st, st1;   // st, st1: dwords around the stored checksum
                     u32x4 w[kSmallK + 1];
                 };
                 auto load_oct = [&](uint64_t o, Oct& t) {
@@ -1891,7 +1891,13 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
                     const uint64_t A = line_base(t.S);
                     const uint64_t p0 = A + gl * 16;
                     const uint64_t safe = t.steps ? A : dummy;
-                    t.st = d.vstat && t.steps ? load_u32_any(t.S - 4) : 0u;
+                    t.st = t.st1 = 0u;   // joined at use: a join here would wait for them
+                    if (d.vstat && t.steps) {
+                        typedef const __attribute__((address_space(1))) uint32_t g32s;
+                        const uint64_t sa = (t.S - 4) & ~uint64_t(3);
+                        t.st = *reinterpret_cast<g32s*>(sa);
+                        t.st1 = *reinterpret_cast<g32s*>(sa + 4);
+                    }
     #pragma unroll
                     for (int k = 0; k <= kSmallK; k++) {
                         const uint64_t a = p0 + uint64_t(k) * kStep;
@@ -1943,7 +1949,7 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
                     pu3 = u3;
                     ppad = uint32_t((A + uint64_t(cur.steps) * kStep) - cur.E);
                     pix = cur.ix;
-                    pst = cur.st;
+                    pst = __builtin_amdgcn_alignbyte(cur.st1, cur.st, uint32_t(cur.S - 4) & 3);
                     flush();
                     cur = nxt;
                 }
@@ -2004,7 +2010,16 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
                 Abuf[j] = ldf(1 + j < kt0 ? 1 + j : 0);
             // the stored checksum (records mode) behind the data loads; read at
             // the octet's end
-            const uint32_t stv = d.vstat && steps ? load_u32_any(S - 4) : 0u;
+            // (its two dwords are loaded here and joined at the octet's end:
+            // joining them here would wait for every load above before the
+            // previous octet's fold, exposing one memory latency per octet)
+            typedef const __attribute__((address_space(1))) uint32_t g32s;
+            uint32_t sw0 = 0u, sw1 = 0u;
+            if (d.vstat && steps) {
+                const uint64_t sa = (S - 4) & ~uint64_t(3);
+                sw0 = *reinterpret_cast<g32s*>(sa);
+                sw1 = *reinterpret_cast<g32s*>(sa + 4);
+            }
             __builtin_amdgcn_sched_barrier(0);
             flush();
 
@@ -2100,7 +2115,7 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
             pu3 = u3;
             ppad = uint32_t((A + uint64_t(eff) * kStep) - E);
             pix = ix;
-            pst = stv;
+            pst = __builtin_amdgcn_alignbyte(sw1, sw0, uint32_t(S - 4) & 3);
     };
 
     // Work split.  Waves given equal shares of the long bins finish in the
