@@ -153,6 +153,9 @@ VARIANTS = {
     "sk0": ["RAMCRC_AGE_SKEW=0"],
     "sk30": ["RAMCRC_AGE_SKEW=30"],
     "sk50": ["RAMCRC_AGE_SKEW=50"],
+    "oc2": ["RAMCRC_OCTET_COST=2"],
+    "sk80": ["RAMCRC_AGE_SKEW=80"],
+    "oc6": ["RAMCRC_OCTET_COST=6"],
     "sk120": ["RAMCRC_AGE_SKEW=120"],
     "nobatch": ["RAMCRC_STEP_BATCH=0"],
 

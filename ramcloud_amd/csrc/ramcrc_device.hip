@@ -871,16 +871,25 @@ constexpr int kPU = RAMCRC_PU;             // ping-pong depth (pipelined bins)
 #define RAMCRC_TINY_PROBE 0  // A/B only: conflict-free lookup addresses, wrong CRCs
 #endif
 constexpr uint32_t kNoIdx = 0xFFFFFFFFu;   // empty slot
-constexpr uint64_t kOctetCost = 4;         // per-octet overhead in step units (work split)
+#ifndef RAMCRC_OCTET_COST
+#define RAMCRC_OCTET_COST 4
+#endif
+constexpr uint64_t kOctetCost = RAMCRC_OCTET_COST;   // per-octet overhead in step units (work split)
 #ifndef RAMCRC_AGE_SKEW
-#define RAMCRC_AGE_SKEW 80
+#define RAMCRC_AGE_SKEW 140
+#endif
+#ifndef RAMCRC_AGE_SKEW_REC
+#define RAMCRC_AGE_SKEW_REC 80
 #endif
 // long bins: share of a wave of age rank r (slot / 4) in 1/2000 of an equal
-// share: 2000 + skew * (3 - 2 r), i.e. +-12 % at the outer ranks for skew 80
-constexpr int kAgeSkew = RAMCRC_AGE_SKEW;
-__host__ __device__ constexpr uint64_t age_weight(uint32_t r)
+// share: 2000 + skew * (3 - 2 r), i.e. +-21 % at the outer ranks for skew
+// 140.  Same-box A/B (profiles/r03/long/ab_skew*.txt): plain batches gain up
+// to skew 120-160 (config-3 mix +4 % over 80), replay verify (records mode)
+// loses from 120 on (-3 %), so records mode keeps 80.
+constexpr int kAgeSkew = RAMCRC_AGE_SKEW, kAgeSkewRec = RAMCRC_AGE_SKEW_REC;
+__host__ __device__ constexpr uint64_t age_weight(uint32_t r, int skew)
 {
-    return uint64_t(2000 + kAgeSkew * (3 - 2 * int(r)));
+    return uint64_t(2000 + skew * (3 - 2 * int(r)));
 }
 static_assert(RAMCRC_ENT_WAVES % 4 == 0, "age ranks of four waves");
 #ifndef RAMCRC_BIN_PER
@@ -2135,12 +2144,13 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
         const uint64_t P0 = I0 + T * blk / nblk, PT = I0 + T * (blk + 1) / nblk - P0;
         const uint32_t slot = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
         // cumulative weight of the slots before `slot` (4 slots per age rank)
-        auto cum = [](uint32_t sl) -> uint64_t {
+        const int skew = d.vstat ? kAgeSkewRec : kAgeSkew;
+        auto cum = [&](uint32_t sl) -> uint64_t {
             uint64_t c = 0;
 #pragma unroll
             for (uint32_t r = 0; r < kEntWaves / 4; r++) {
                 const uint32_t n = sl > 4 * r ? (sl - 4 * r < 4 ? sl - 4 * r : 4) : 0;
-                c += uint64_t(n) * age_weight(r);
+                c += uint64_t(n) * age_weight(r, skew);
             }
             return c;
         };
