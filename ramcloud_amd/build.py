@@ -155,6 +155,8 @@ VARIANTS = {
     "sk50": ["RAMCRC_AGE_SKEW=50"],
     "oc2": ["RAMCRC_OCTET_COST=2"],
     "sk80": ["RAMCRC_AGE_SKEW=80"],
+    "ss7": ["RAMCRC_SYNC_STAGE_KIB=7"],
+    "sh5_ss7": ["RAMCRC_SYNC_HOPS=5", "RAMCRC_SYNC_STAGE_KIB=7"],
     "oc6": ["RAMCRC_OCTET_COST=6"],
     "sk120": ["RAMCRC_AGE_SKEW=120"],
     "nobatch": ["RAMCRC_STEP_BATCH=0"],
