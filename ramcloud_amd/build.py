@@ -156,6 +156,7 @@ VARIANTS = {
     "oc2": ["RAMCRC_OCTET_COST=2"],
     "sk80": ["RAMCRC_AGE_SKEW=80"],
     "ss7": ["RAMCRC_SYNC_STAGE_KIB=7"],
+    "ss9": ["RAMCRC_SYNC_STAGE_KIB=9"],
     "sh5_ss7": ["RAMCRC_SYNC_HOPS=5", "RAMCRC_SYNC_STAGE_KIB=7"],
     "oc6": ["RAMCRC_OCTET_COST=6"],
     "sk120": ["RAMCRC_AGE_SKEW=120"],

@@ -2998,7 +2998,7 @@ constexpr uint32_t kNoStart = 0xFFFFFFFFu;
 #define RAMCRC_SYNC_PER 8
 #endif
 #ifndef RAMCRC_SYNC_STAGE_KIB
-#define RAMCRC_SYNC_STAGE_KIB 9
+#define RAMCRC_SYNC_STAGE_KIB 7
 #endif
 constexpr int kSyncHops = RAMCRC_SYNC_HOPS;         // hops a guess must survive
 constexpr int kSyncPer = RAMCRC_SYNC_PER;           // candidates per lane per round
