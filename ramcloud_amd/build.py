@@ -157,6 +157,9 @@ VARIANTS = {
     "sk80": ["RAMCRC_AGE_SKEW=80"],
     "ss7": ["RAMCRC_SYNC_STAGE_KIB=7"],
     "ss9": ["RAMCRC_SYNC_STAGE_KIB=9"],
+    "ps15": ["RAMCRC_PART_SHIFT=15"],
+    "ps17": ["RAMCRC_PART_SHIFT=17"],
+    "fw8": ["RAMCRC_FIX_WIN_KIB=8"],
     "sh5_ss7": ["RAMCRC_SYNC_HOPS=5", "RAMCRC_SYNC_STAGE_KIB=7"],
     "oc6": ["RAMCRC_OCTET_COST=6"],
     "sk120": ["RAMCRC_AGE_SKEW=120"],
