@@ -40,9 +40,11 @@ enum {
     RAMCRC_ERCCL = -5,    /* RCCL failure or RCCL unavailable (multi-GPU shard) */
     RAMCRC_EREFUSED = -6, /* a launch found more chunks than the context's scratch holds and
                              wrote none of its outputs (see ramcrc_ctx_check) */
-    RAMCRC_EINTERNAL = -7 /* a small-entry launch found its bin layout inconsistent with the
+    RAMCRC_EINTERNAL = -7, /* a small-entry launch found its bin layout inconsistent with the
                              entries it binned; its outputs are unspecified (an internal
                              invariant; never expected -- see ramcrc_ctx_check) */
+    RAMCRC_EPEER = -8     /* multi-GPU shard: this rank's part of the step succeeded but
+                             another rank's failed; that rank's segments read 0xFFFFFFFF */
 };
 
 /* Output flag: apply the final inversion (Crc32C::getResult, src/Crc32C.h:247).
@@ -331,12 +333,28 @@ int ramcrc_shard_info(const ramcrc_shard* shard, int k, int* rank, int* device, 
  * NULL, the shard's own result buffers do (ramcrc_shard_results).  flags:
  * RAMCRC_FINALIZE as for ramcrc_segments_device.  Asynchronous on the
  * shard's streams; a single-process shard issues the ranks' collectives in
- * one RCCL group. */
+ * one RCCL group.  Every rank must pass the same nseg.
+ *
+ * Liveness (ramcloud_amd/csrc/shard_plan.h): no rank leaves a step before a
+ * collective its peers wait in.  A step whose nseg exceeds every earlier one
+ * grows the shard's internal buffers on every rank and then exchanges one
+ * status word per rank, synchronously; if any rank could not allocate, every
+ * rank returns an error before the data collective (RAMCRC_ENOMEM on that
+ * rank, RAMCRC_EPEER on the others).  Any other failure of a rank (bad
+ * arguments, a failed launch) is returned by it, and it still joins the
+ * all-gather with its segments' slots set to 0xFFFFFFFF; its status word
+ * travels with the CRCs, so its peers' next ramcrc_shard_sync returns
+ * RAMCRC_EPEER. */
 int ramcrc_shard_segments(ramcrc_shard* shard, const void* const* d_shard, uint64_t seg_bytes,
                           uint64_t nseg, uint32_t* const* d_all, uint32_t flags);
 
-/* Wait for every local rank's stream; RAMCRC_ERCCL if RCCL reported an
- * asynchronous error. */
+/* Wait for every local rank's stream.  Returns RAMCRC_ERCCL if RCCL reported
+ * an asynchronous error, a device launch's refusal (ramcrc_ctx_check), this
+ * rank's own failure of the last step, RAMCRC_EPEER when the last step's
+ * gathered status words show that another rank failed (the results then hold
+ * 0xFFFFFFFF for its segments), RAMCRC_OK when every CRC of the last step is
+ * valid.  Device-side refusals are only seen by the rank that hit them (the
+ * uniform-segment scan never refuses). */
 int ramcrc_shard_sync(ramcrc_shard* shard);
 
 /* Copy local rank k's gathered CRCs of the last step (when it ran with d_all

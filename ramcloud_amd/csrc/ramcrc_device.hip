@@ -2624,7 +2624,13 @@ int bin_begin(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_large, 
     if (rc)
         return rc;
     *so = Sorted{c->bins, c->sdesc, c->sidx, c->sinit, c->status, c->sorted_cap, c->bin_par};
-    (void)hipGetLastError();   // clear a stale error: the next one is this launch's
+    // Every launch of this library checks its own error right after it (the
+    // timed ScanTimer::launch calls included), so an error pending here was left
+    // by a caller's own HIP call on this thread (torch's pointer probes leave
+    // such errors behind).  It is recorded for ramcrc_last_hip_error and cleared,
+    // not reported as this launch's failure.
+    if (hipError_t stale = hipGetLastError(); stale != hipSuccess)
+        t_last_hip = int(stale);
     hipLaunchKernelGGL(k_bin_count<kMode>, dim3(bin_grid(c, d.n)), dim3(kThreads), 0, s, d, *so,
                        skip_large);
     HIPCHK(hipGetLastError());
@@ -4372,6 +4378,7 @@ const char* ramcrc_strerror(int code)
     case RAMCRC_ERCCL: return "rccl failure";
     case RAMCRC_EREFUSED: return "launch refused: chunk scratch too small (ramcrc_ctx_reserve)";
     case RAMCRC_EINTERNAL: return "launch refused: inconsistent small-entry bin layout";
+    case RAMCRC_EPEER: return "another rank of the shard failed this step";
     default: return "unknown error";
     }
 }

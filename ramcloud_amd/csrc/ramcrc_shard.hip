@@ -33,6 +33,8 @@
 #include "ramcrc.h"
 #include "shard_plan.h"
 
+static_assert(ramcrc_shard_plan::kPeerFailed == RAMCRC_EPEER, "peer failure code");
+
 namespace {
 
 struct Rccl {
@@ -123,6 +125,8 @@ struct Local {
     uint64_t gather_cap = 0;
     uint32_t* all = nullptr;      // nseg (results when the caller passes no d_all)
     uint64_t all_cap = 0;
+    uint32_t* status = nullptr;   // nranks words: every rank's status of the last exchange
+    uint32_t* h_status = nullptr; // pinned host copy read by ramcrc_shard_sync
     uint64_t last_nseg = 0;
     bool last_internal = false;
     int failed = 0;               // a step's failure after its collective was enqueued
@@ -147,18 +151,19 @@ int grow(uint32_t** p, uint64_t* cap, uint64_t n)
 {
     if (*cap >= n && *p)
         return RAMCRC_OK;
-    if (*p) {
-        HIPCHK_S(hipDeviceSynchronize());
-        HIPCHK_S(hipFree(*p));
-        *p = nullptr;
-        *cap = 0;
-    }
-    const uint64_t want = n < 256 ? 256 : n;
-    if (hipMalloc(reinterpret_cast<void**>(p), want * sizeof(uint32_t)) != hipSuccess) {
-        *p = nullptr;
+    // the new buffer first: a failed growth keeps the old one
+    uint32_t* q = nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&q), n * sizeof(uint32_t)) != hipSuccess)
         return RAMCRC_ENOMEM;
+    if (*p) {
+        if (hipDeviceSynchronize() != hipSuccess) {
+            (void)hipFree(q);
+            return RAMCRC_EHIP;
+        }
+        (void)hipFree(*p);
     }
-    *cap = want;
+    *p = q;
+    *cap = n;
     return RAMCRC_OK;
 }
 
@@ -166,6 +171,7 @@ int grow(uint32_t** p, uint64_t* cap, uint64_t n)
 
 struct ramcrc_shard {
     int nranks = 0;
+    uint64_t capacity = 0;   // watermark of every local rank's gather/all buffers (shard_plan.h)
     std::vector<Local> local;
     std::mutex mu;
 };
@@ -181,6 +187,13 @@ int finish_create(ramcrc_shard* sh)
         int rc = ramcrc_ctx_create(l.device, &l.ctx);
         if (rc)
             return rc;
+        const size_t sb = size_t(sh->nranks) * sizeof(uint32_t);
+        if (hipMalloc(reinterpret_cast<void**>(&l.status), sb) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void**>(&l.h_status), sb, hipHostMallocDefault) !=
+                hipSuccess)
+            return RAMCRC_ENOMEM;
+        HIPCHK_S(hipMemset(l.status, 0, sb));
+        memset(l.h_status, 0, sb);
     }
     return RAMCRC_OK;
 }
@@ -203,15 +216,62 @@ struct StepOps {
             return RAMCRC_EINVAL;
         return RAMCRC_OK;
     }
-    int reserve(int k, uint64_t gather_elems, uint64_t all_elems)
+    uint64_t capacity() const { return sh->capacity; }
+    void set_capacity(uint64_t c) { sh->capacity = c; }
+    int reserve(int k, uint64_t elems)
     {
         Local& l = sh->local[k];
         DevGuard g(l.device);
-        l.failed = 0;
-        int rc = gather_elems ? grow(&l.gather, &l.gather_cap, gather_elems) : RAMCRC_OK;
-        if (!rc && all_elems)
-            rc = grow(&l.all, &l.all_cap, all_elems);
+        int rc = grow(&l.gather, &l.gather_cap, elems);
+        if (!rc)
+            rc = grow(&l.all, &l.all_cap, elems);
         return rc;
+    }
+    // status[rank] = rc on local rank k's stream
+    int put_status(int k, int rc)
+    {
+        Local& l = sh->local[k];
+        DevGuard g(l.device);
+        HIPCHK_S(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(l.status + l.rank), rc, 1,
+                                   l.stream));
+        return RAMCRC_OK;
+    }
+    int all_gather_status(int k)
+    {
+        Local& l = sh->local[k];
+        RCCLCHK(r, r->all_gather(l.status + l.rank, l.status, 1, ncclUint32, l.comm, l.stream),
+                "ncclAllGather(status)");
+        return RAMCRC_OK;
+    }
+    // One status word per rank, exchanged and read back before returning.
+    int agree(const int* st)
+    {
+        const int nlocal = int(sh->local.size());
+        int own = 0;
+        for (int k = 0; k < nlocal; k++) {
+            const int prc = put_status(k, st[k]);
+            if (!own)
+                own = st[k] ? st[k] : prc;
+        }
+        int rc = group_start();
+        if (rc)
+            return rc;
+        for (int k = 0; k < nlocal && !rc; k++)
+            rc = all_gather_status(k);
+        const int ge = group_end();
+        if (rc || ge)
+            return rc ? rc : ge;
+        int peer = 0;
+        for (int k = 0; k < nlocal; k++) {
+            Local& l = sh->local[k];
+            DevGuard g(l.device);
+            HIPCHK_S(hipMemcpyAsync(l.h_status, l.status, size_t(sh->nranks) * sizeof(uint32_t),
+                                    hipMemcpyDeviceToHost, l.stream));
+            HIPCHK_S(hipStreamSynchronize(l.stream));
+            if (!peer)
+                peer = ramcrc_shard_plan::peer_status(0, l.h_status, sh->nranks);
+        }
+        return own ? own : peer;
     }
     int scan(int k, uint64_t lo, uint64_t hi, bool caller, uint64_t off)
     {
@@ -388,6 +448,10 @@ int ramcrc_shard_destroy(ramcrc_shard* sh)
             (void)hipFree(l.gather);
         if (l.all)
             (void)hipFree(l.all);
+        if (l.status)
+            (void)hipFree(l.status);
+        if (l.h_status)
+            (void)hipHostFree(l.h_status);
         if (l.stream)
             (void)hipStreamDestroy(l.stream);
     }
@@ -424,8 +488,10 @@ int ramcrc_shard_segments(ramcrc_shard* sh, const void* const* d_shard, uint64_t
     std::lock_guard<std::mutex> lk(sh->mu);
     const int nlocal = int(sh->local.size());
     std::vector<int> ranks(nlocal);
-    for (int k = 0; k < nlocal; k++)
+    for (int k = 0; k < nlocal; k++) {
         ranks[k] = sh->local[k].rank;
+        sh->local[k].failed = 0;
+    }
     StepOps ops{sh, r, d_shard, d_all, seg_bytes, flags};
     const int rc = ramcrc_shard_plan::run_step(ops, nlocal, ranks.data(), sh->nranks, nseg,
                                                d_all != nullptr);
@@ -443,6 +509,9 @@ int ramcrc_shard_sync(ramcrc_shard* sh)
     const Rccl* r = rccl();
     for (Local& l : sh->local) {
         DevGuard g(l.device);
+        // every rank's status word of the last exchange (shard_plan.h)
+        HIPCHK_S(hipMemcpyAsync(l.h_status, l.status, size_t(sh->nranks) * sizeof(uint32_t),
+                                hipMemcpyDeviceToHost, l.stream));
         HIPCHK_S(hipStreamSynchronize(l.stream));
         if (r && l.comm) {
             ncclResult_t ae = ncclSuccess;
@@ -453,8 +522,10 @@ int ramcrc_shard_sync(ramcrc_shard* sh)
         int rc = ramcrc_ctx_check(l.ctx, l.stream);
         if (rc)
             return rc;
-        if (l.failed)
-            return l.failed;   // its slots of the last step were poisoned
+        // own failure (its slots of the last step were poisoned), else a peer's
+        rc = ramcrc_shard_plan::peer_status(l.failed, l.h_status, sh->nranks);
+        if (rc)
+            return rc;
     }
     return RAMCRC_OK;
 }

@@ -21,9 +21,12 @@ FINALIZE = 1
 
 _ERRORS = {0: "ok", -1: "invalid argument", -2: "out of memory", -3: "HIP error",
            -4: "no usable device", -5: "RCCL error", -6: "launch refused (scratch too small)",
-           -7: "launch refused (inconsistent bin layout)"}
+           -7: "launch refused (inconsistent bin layout)",
+           -8: "another shard rank failed"}
 
+ENOMEM = -2
 EINTERNAL = -7
+EPEER = -8
 
 # ramcrc_ctx_set_option options (include/ramcrc.h)
 OPT_SERIAL_WALK = 1

@@ -114,9 +114,11 @@ class RecoveryVerify:
         #   entries_cap  fixed table; a walk that overflows it marks the
         #                segment TABLE_FULL (never OK) and check() raises;
         #   min_entry    fixed table sized for entries of at least that size;
-        #   neither      a table for 128-byte entries on average that
-        #                verify(check=True) grows (and walks again) when a walk
-        #                finds more records -- at most once per batch shape.
+        #   neither      a table for 128-byte entries on average that verify()
+        #                grows (and walks again) when a walk finds more
+        #                records -- at most once per batch shape.  verify() then
+        #                waits for the walk's record count on every call, with
+        #                or without check=True: no segment is left TABLE_FULL.
         self.grow = entries_cap is None and min_entry is None
         if entries_cap is None:
             per = self.GROW_START_ENTRY if self.grow else min_entry
@@ -146,10 +148,13 @@ class RecoveryVerify:
     def verify(self, d_segments, d_certs, stream=None, check=False):
         """Walk + per-record verify.  check=True waits for the stream and raises
         if the record table overflowed (some segment not verified) or a launch
-        was refused; a growing table (no entries_cap / min_entry given) is
-        first enlarged to the walked record count and the batch walked again."""
+        was refused.  A growing table (no entries_cap / min_entry given) always
+        reads the walked record count back (a host sync), and when the walk
+        found more records than the table holds it is enlarged and the batch
+        walked again, so that verify(check=False) never returns segments left
+        TABLE_FULL; fixed tables never sync unless check=True."""
         self.walk(d_segments, d_certs, stream)
-        if check and self.grow:
+        if self.grow:
             self.ctx.check(stream)
             n = int(self.n_entries.item())
             if n > self.entries.shape[0]:

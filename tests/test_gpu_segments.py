@@ -145,6 +145,27 @@ def test_walk_tombstone_only_default_table(ramcrc, oracle_mod, golden):
 
 
 @pytest.mark.gpu
+def test_walk_small_records_default_table_no_check(ramcrc, oracle_mod):
+    """Segments of 64-byte-value objects (101-byte entries, below the 128 bytes
+    the growing table starts from) with the default table and check=False:
+    verify() itself grows the table and walks again, so every segment is
+    verified (OK, exact counts), none is left TABLE_FULL."""
+    import torch
+    cap, nseg = 1 << 18, 8
+    buf, certs, counts = segments.object_segments_host(nseg, cap, 64)
+    ctx = ramcrc.Context(0)
+    rv = segments.RecoveryVerify(ctx, nseg, cap)
+    assert rv.entries.shape[0] < counts.sum()
+    d = torch.from_numpy(buf).cuda()
+    dc = torch.from_numpy(np.ascontiguousarray(certs).view(np.int32)).cuda()
+    st = rv.verify(d, dc).cpu().numpy().view(np.uint32)
+    assert (st[:, 0] == segments.SEG_OK).all()
+    assert np.array_equal(st[:, 2], counts)
+    assert (st[:, 3] == 0).all()
+    rv.check()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("value_len", [64, 1024, 8192, 100000])
 def test_parallel_walk_8mib_vs_oracle(ramcrc, oracle_mod, value_len):
     """8 MiB object segments (128 parts of the parallel walk) at the

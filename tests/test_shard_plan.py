@@ -13,7 +13,7 @@ from conftest import ROOT
 
 def test_shard_plan_host(tmp_path):
     exe = tmp_path / "shard_plan_test"
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-Wall", "-Werror",
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-Wall", "-Werror", "-pthread",
                            "-I" + os.path.join(ROOT, "ramcloud_amd", "csrc"),
                            os.path.join(ROOT, "tests", "cpp", "shard_plan_test.cc"), "-o", str(exe)])
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)

@@ -1,0 +1,12 @@
+# Round 4: shard liveness/status tests and the new segment test first, then the
+# whole GPU suite, smoke, the default bench line and config 4 at N = 1 with the
+# full gathered-CRC check (library built here, shipped prebuilt).
+set -o pipefail
+OUT=gpurun_out/${1:-r04}
+mkdir -p "$OUT"
+python -c "import ramcloud_amd.ramcrc as r; print(r.lib().ramcrc_build_info().decode())" > "$OUT/build_info.txt" 2>&1 || exit 1
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_shard.py tests/test_gpu_segments.py > "$OUT/pytest_new.log" 2>&1 || exit 1
+timeout -k 10 900 python -u -m pytest -x -v --timeout 240 --timeout-method thread -m gpu tests > "$OUT/pytest_gpu.log" 2>&1 || exit 1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || exit 1
+timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 1
+timeout -k 10 300 python bench.py --config recovery > "$OUT/recovery.json" 2> "$OUT/recovery.err" || exit 1
