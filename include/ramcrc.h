@@ -43,14 +43,30 @@ enum {
     RAMCRC_EINTERNAL = -7, /* a small-entry launch found its bin layout inconsistent with the
                              entries it binned; its outputs are unspecified (an internal
                              invariant; never expected -- see ramcrc_ctx_check) */
-    RAMCRC_EPEER = -8     /* multi-GPU shard: this rank's part of the step succeeded but
+    RAMCRC_EPEER = -8,    /* multi-GPU shard: this rank's part of the step succeeded but
                              another rank's failed; that rank's segments read 0xFFFFFFFF */
+    RAMCRC_EORDER = -9    /* a RAMCRC_ORDERED batch was not in log order (entries overlap,
+                             are out of order, or leave a gap of 4 KiB or more between
+                             neighbours): nothing was written (see ramcrc_ctx_check) */
 };
 
 /* Output flag: apply the final inversion (Crc32C::getResult, src/Crc32C.h:247).
  * Without it the raw running state (Crc32C::result, :259) is returned, which
  * callers use to keep chaining (src/LogDigest.cc:75-80, src/Segment.cc:677-681). */
 #define RAMCRC_FINALIZE 1u
+
+/* Input flag of ramcrc_batch_device / ramcrc_entries_device: the buffers are
+ * log entries in log order -- sorted by offset, not overlapping, neighbours
+ * less than 4 KiB apart (the bytes between them readable), as the entries of a
+ * segment (src/Segment.cc:197-228), the objects a replay walks
+ * (src/ObjectManager.cc:585-700) or a write batch appended in order
+ * (src/ObjectManager.cc:1274-1297) lie.  The batch is then checksummed as one
+ * byte stream in a single pass (every covered byte read once, entry ends
+ * resolved on the fly) instead of entry by entry.  Results are identical.
+ * The order is verified on the device; a batch that breaks it is refused
+ * (nothing written, RAMCRC_EORDER from ramcrc_ctx_check).  Ignored when d_init
+ * is not NULL (per-entry initial states take the general path). */
+#define RAMCRC_ORDERED 2u
 
 /* ---------------------------------------------------------------- host --- */
 

@@ -95,6 +95,8 @@ struct alignas(16) DeviceTables {
     uint32_t post[256 * 128 + 128];
     uint32_t xmeta[5 * 64 + 1];   // k_seg_walk: x^(8d), d = 0 .. 320 (one batch of metadata)
     uint32_t xbyte[4][256];       // x^(8 * b * 256^j): x^(8d) for any 32-bit d in 4 factors
+    alignas(16) OpTable xinv128;  // k_stream: X^-128 (an entry's value moved back from the step end)
+    alignas(16) uint32_t xff[132];   // k_stream: X^d(0xFFFFFFFF), d = 0 .. 128 (the initial state)
     // k_entries' long phase (group_fold, flush_batch, head and tail steps),
     // laid out as in LDS from kX4Off on, so one fill copies them all:
     struct alignas(16) LongTabs {
@@ -145,6 +147,14 @@ constexpr DeviceTables make_device_tables()
             t.xbyte[j][b] = acc;
             acc = ramcrc::mulmod(acc, base);
         }
+    }
+    {
+        const uint32_t c = ramcrc::xinv8pow(128);
+        for (int k = 0; k < 4; k++)
+            for (uint32_t b = 0; b < 256; b++)
+                t.xinv128.t[k][b] = ramcrc::mulmod(b << (8 * k), c);
+        for (int dd = 0; dd <= 128; dd++)
+            t.xff[dd] = ramcrc::mulmod(0xFFFFFFFFu, ramcrc::xpow8(uint64_t(dd)));
     }
     t.lt.x4 = t.comb[0];
     t.lt.x16 = t.comb[1];
@@ -2360,6 +2370,8 @@ __global__ __launch_bounds__(kThreads) void k_plan_scan(Plan pl)
         pl.group_pref[pl.ngroups] = carry_s;
 }
 
+#include "stream.h"
+
 // Test hook (RAMCRC_OPT_TEST_DIRTY_BINS): corrupt the histogram of a binning
 // sequence between its count and scatter passes, as a stale histogram would.
 __global__ void k_test_dirty_bins(BinTable* bt, uint32_t par, uint32_t bin, uint32_t add)
@@ -2372,7 +2384,7 @@ __global__ void k_test_dirty_bins(BinTable* bt, uint32_t par, uint32_t bin, uint
 // to status[1] for the host to read.
 __global__ void k_status_take(uint32_t* status)
 {
-    status[1] = atomicAnd(status, ~(kStatusSticky | kStatusBins));
+    status[1] = atomicAnd(status, ~(kStatusSticky | kStatusBins | kStatusOrder));
 }
 
 // ------------------------------------------------------------ host side
@@ -2458,6 +2470,10 @@ struct ramcrc_ctx {
     uint64_t walk_pool_used_cap = 0;
     bool serial_walk = false;   // RAMCRC_OPT_SERIAL_WALK
     uint32_t walk_pshift = 0;   // RAMCRC_OPT_WALK_PART_SHIFT; 0: kPartShift
+    // ordered-stream scratch (k_stream*): 4 words per span + the refusal word
+    uint32_t* stream_scr = nullptr;
+    uint64_t stream_scr_cap = 0;
+    uint32_t stream_seq = 0;
     // benchmark timing of the scan kernels
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_used, ev_free;
@@ -2699,6 +2715,54 @@ int launch_planned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s)
                            uint64_t(0));
     HIPCHK(hipGetLastError());
     return bin_finish<kMode>(c, d, s, 1, so);
+}
+
+// Ordered batch (RAMCRC_ORDERED): k_stream_prep -> k_stream -> k_stream_fix
+// (stream.h).  Every launch gets a new sequence number, so a refusal word
+// left by an earlier launch never stops a later one.
+int launch_stream(ramcrc_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                  uint32_t* out, uint64_t n, uint32_t flags, hipStream_t s)
+{
+    if (n >= (1ull << 32) - 1)
+        return RAMCRC_EINVAL;   // 32-bit entry indices
+    const uint32_t nspan = uint32_t(c->ncu) * kStreamGroups;
+    const uint64_t words = 4ull * nspan + 4;
+    if (c->stream_scr_cap < words) {
+        int rc = grow_device(reinterpret_cast<void**>(&c->stream_scr), &c->stream_scr_cap, words,
+                             sizeof(uint32_t));
+        if (rc)
+            return rc;
+        HIPCHK(hipMemset(c->stream_scr, 0, c->stream_scr_cap * sizeof(uint32_t)));
+        c->stream_seq = 0;
+    }
+    StreamDesc d{};
+    d.base = base;
+    d.off = off;
+    d.len = len;
+    d.n = n;
+    d.out = out;
+    d.flags = flags;
+    d.nspan = nspan;
+    d.seq = ++c->stream_seq == 0 ? ++c->stream_seq : c->stream_seq;   // never 0 (the initial word)
+    d.first_ev = c->stream_scr;
+    d.span_t = c->stream_scr + nspan;
+    d.xe_val = c->stream_scr + 2 * uint64_t(nspan);
+    d.xe_idx = c->stream_scr + 3 * uint64_t(nspan);
+    d.bad_seq = c->stream_scr + 4 * uint64_t(nspan);
+    d.status = c->status;
+    uint64_t pg = (n + 255) / 256;
+    if (pg > uint64_t(c->ncu) * 8)
+        pg = uint64_t(c->ncu) * 8;
+    hipLaunchKernelGGL(k_stream_prep, dim3(pg), dim3(256), 0, s, d);
+    HIPCHK(hipGetLastError());
+    {
+        ScanTimer t(c, s);
+        t.launch(k_stream, dim3(c->ncu), dim3(kStreamWaves * kWaveSize), d);
+    }
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_stream_fix, dim3((nspan + 255) / 256), dim3(256), 0, s, d);
+    HIPCHK(hipGetLastError());
+    return RAMCRC_OK;
 }
 
 // ------------------------------------------------------------ segment walk
@@ -4379,6 +4443,7 @@ const char* ramcrc_strerror(int code)
     case RAMCRC_EREFUSED: return "launch refused: chunk scratch too small (ramcrc_ctx_reserve)";
     case RAMCRC_EINTERNAL: return "launch refused: inconsistent small-entry bin layout";
     case RAMCRC_EPEER: return "another rank of the shard failed this step";
+    case RAMCRC_EORDER: return "ordered batch refused: entries overlap, are out of order or leave a gap of 4 KiB or more";
     default: return "unknown error";
     }
 }
@@ -4479,6 +4544,7 @@ int ramcrc_ctx_destroy(ramcrc_ctx* c)
     if (c->walk_pool_owner) (void)hipFree(c->walk_pool_owner);
     if (c->walk_blocks) (void)hipFree(c->walk_blocks);
     if (c->walk_pool_used) (void)hipFree(c->walk_pool_used);
+    if (c->stream_scr) (void)hipFree(c->stream_scr);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -4648,6 +4714,8 @@ int ramcrc_ctx_check(ramcrc_ctx* c, void* stream)
     HIPCHK(hipMemcpy(&st, c->status + 1, sizeof(uint32_t), hipMemcpyDeviceToHost));
     if (st & kStatusBins)
         return RAMCRC_EINTERNAL;
+    if (st & kStatusOrder)
+        return RAMCRC_EORDER;
     return (st & kStatusSticky) ? RAMCRC_EREFUSED : RAMCRC_OK;
 }
 
@@ -4726,6 +4794,9 @@ int ramcrc_batch_device(ramcrc_ctx* c, const void* d_base, const uint64_t* d_off
     d.init = d_init;
     d.out = d_out;
     d.flags = flags;
+    if ((flags & RAMCRC_ORDERED) && !d_init)
+        return launch_stream(c, d.base, d_off, d_len, d_out, n, flags,
+                             reinterpret_cast<hipStream_t>(stream));
     return launch_planned<kTable>(c, d, reinterpret_cast<hipStream_t>(stream));
 }
 
@@ -4749,6 +4820,8 @@ int ramcrc_entries_device(ramcrc_ctx* c, const void* d_base, const uint64_t* d_o
     d.init = d_init;
     d.out = d_out;
     d.flags = flags;
+    if ((flags & RAMCRC_ORDERED) && !d_init)
+        return launch_stream(c, d.base, d_off, d_len, d_out, n, flags, s);
     return launch_binned<kTable>(c, d, s, 0);
 }
 

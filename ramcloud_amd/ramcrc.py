@@ -18,15 +18,18 @@ _c = ctypes
 _lib = None
 
 FINALIZE = 1
+ORDERED = 2   # RAMCRC_ORDERED: the batch is log entries in log order
 
 _ERRORS = {0: "ok", -1: "invalid argument", -2: "out of memory", -3: "HIP error",
            -4: "no usable device", -5: "RCCL error", -6: "launch refused (scratch too small)",
            -7: "launch refused (inconsistent bin layout)",
-           -8: "another shard rank failed"}
+           -8: "another shard rank failed",
+           -9: "ordered batch refused (entries not in log order)"}
 
 ENOMEM = -2
 EINTERNAL = -7
 EPEER = -8
+EORDER = -9
 
 # ramcrc_ctx_set_option options (include/ramcrc.h)
 OPT_SERIAL_WALK = 1
@@ -317,17 +320,20 @@ class Context:
         _check(rc, "ramcrc_segments_device")
         return out
 
-    def batch(self, data, off, length, out, init=None, finalize=True, stream=None):
+    def batch(self, data, off, length, out, init=None, finalize=True, stream=None, ordered=False):
+        """ordered=True: RAMCRC_ORDERED (entries in log order; one stream pass)."""
         n = off.numel()
+        fl = (FINALIZE if finalize else 0) | (ORDERED if ordered else 0)
         rc = lib().ramcrc_batch_device(self._h, _ptr(data), _ptr(off), _ptr(length), _ptr(init),
-                                       _ptr(out), n, FINALIZE if finalize else 0, _stream(stream))
+                                       _ptr(out), n, fl, _stream(stream))
         _check(rc, "ramcrc_batch_device")
         return out
 
-    def entries(self, data, off, length, out, init=None, finalize=True, stream=None):
+    def entries(self, data, off, length, out, init=None, finalize=True, stream=None, ordered=False):
         n = off.numel()
+        fl = (FINALIZE if finalize else 0) | (ORDERED if ordered else 0)
         rc = lib().ramcrc_entries_device(self._h, _ptr(data), _ptr(off), _ptr(length), _ptr(init),
-                                         _ptr(out), n, FINALIZE if finalize else 0, _stream(stream))
+                                         _ptr(out), n, fl, _stream(stream))
         _check(rc, "ramcrc_entries_device")
         return out
 
