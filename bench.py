@@ -805,9 +805,11 @@ def run_append(args, ranks):
     off_t = torch.from_numpy(offs.view(np.int64)).cuda()
     len_t = torch.from_numpy(lens.view(np.int64)).cuda()
     out = torch.zeros(lens.size, dtype=torch.int32, device="cuda")
+    ordered = args.order == "log"
     torch.cuda.synchronize()
     ctx.set_timing(True)
-    elapsed = timed(args.steps, args.warmup, lambda: ctx.assemble_objects(data, off_t, len_t, out),
+    elapsed = timed(args.steps, args.warmup,
+                    lambda: ctx.assemble_objects(data, off_t, len_t, out, ordered=ordered),
                     torch.cuda.synchronize, ranks, on_start=ctx.scan_time)
     scan_ms, _ = ctx.scan_time()
     ctx.set_timing(False)
@@ -823,7 +825,6 @@ def run_append(args, ranks):
         cpu["sample"] += " (object bytes [4, len))"
     ctx.close()
     scan_s = scan_ms / args.steps / 1e3
-    achieved = credited / scan_s / 1e9 if scan_s > 0 else None
     return {
         "metric": "device-resident Object::assembleForLog checksum GB/s over 1M objects "
                   "(100B/1KiB/4KiB Zipf)",
@@ -831,12 +832,12 @@ def run_append(args, ranks):
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-        "config": {"workload": f"{lens.size} objects, {total} bytes", "credited_bytes": credited},
-        "roofline": {"bound": "hbm", "kernel": "k_entries",
-                     "achieved": round(achieved, 1) if achieved else None,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                     "traffic": None, "scan_ms_per_step": round(scan_s * 1e3, 4)},
+        "config": {"workload": f"{lens.size} objects, {total} bytes", "credited_bytes": credited,
+                   "order": ("log order (ramcrc_assemble_objects_ordered_device, verified on the "
+                             "device)" if ordered else "any (binned path)")},
+        "roofline": dict(roofline("k_stream (objects mode)" if ordered else "k_entries", credited,
+                                  scan_s * 1e3, f"append_{lens.size}_mix" + ("_ordered" if ordered else "")),
+                         scan_ms_per_step=round(scan_s * 1e3, 4)),
         "cpu_baseline": cpu,
     }
 

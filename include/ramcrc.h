@@ -393,6 +393,16 @@ int ramcrc_assemble_objects_device(ramcrc_ctx* ctx, void* d_base, const uint64_t
                                    const uint64_t* d_len, uint32_t* d_out, uint64_t n,
                                    void* stream);
 
+/* The same for a write batch whose objects lie in log order (sorted by
+ * offset, not overlapping, neighbours less than 4 KiB apart: packed as
+ * AbstractLog::append lays them out, src/AbstractLog.cc:374-427): the
+ * RAMCRC_ORDERED stream pass checksums all of them in one pass over the
+ * batch's bytes.  Same results; a batch out of order is refused (nothing
+ * checksummed or stamped, RAMCRC_EORDER from ramcrc_ctx_check). */
+int ramcrc_assemble_objects_ordered_device(ramcrc_ctx* ctx, void* d_base, const uint64_t* d_off,
+                                           const uint64_t* d_len, uint32_t* d_out, uint64_t n,
+                                           void* stream);
+
 /* The same for objects in host memory (a write batch still in its RPC
  * buffers): staged through pinned memory, CRCs computed on the GPU, each
  * Header::checksum written back into the host object.  Synchronous. */

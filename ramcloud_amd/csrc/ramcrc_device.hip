@@ -2721,7 +2721,7 @@ int launch_planned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s)
 // (stream.h).  Every launch gets a new sequence number, so a refusal word
 // left by an earlier launch never stops a later one.
 int launch_stream(ramcrc_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len,
-                  uint32_t* out, uint64_t n, uint32_t flags, hipStream_t s)
+                  uint32_t* out, uint64_t n, uint32_t flags, hipStream_t s, bool objects = false)
 {
     if (n >= (1ull << 32) - 1)
         return RAMCRC_EINVAL;   // 32-bit entry indices
@@ -2742,6 +2742,7 @@ int launch_stream(ramcrc_ctx* c, const uint8_t* base, const uint64_t* off, const
     d.n = n;
     d.out = out;
     d.flags = flags;
+    d.obj = objects ? 1u : 0u;
     d.nspan = nspan;
     d.seq = ++c->stream_seq == 0 ? ++c->stream_seq : c->stream_seq;   // never 0 (the initial word)
     d.first_ev = c->stream_scr;
@@ -4369,10 +4370,12 @@ __global__ __launch_bounds__(256) void k_obj_compare(BatchDesc d, ramcrc_seg_sta
 // kernels left in d.out[i], stored little-endian into the object's first 4
 // bytes (which no object's checksum range covers).  Byte stores: objects are
 // packed back to back in a log, so headers are unaligned.
-__global__ __launch_bounds__(256) void k_obj_stamp(BatchDesc d)
+// bad_seq (nullable): an ordered launch's refusal word; when it holds seq the
+// scan wrote nothing, and neither does the stamp.
+__global__ __launch_bounds__(256) void k_obj_stamp(BatchDesc d, const uint32_t* bad_seq, uint32_t seq)
 {
     const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= d.n)
+    if (i >= d.n || (bad_seq && *bad_seq == seq))
         return;
     if (d.len[i] < kObjHeaderBytes) {
         d.out[i] = 0;
@@ -5201,7 +5204,44 @@ int ramcrc_assemble_objects_device(ramcrc_ctx* c, void* d_base, const uint64_t* 
     rc = launch_planned<kObjects>(c, d, s);
     if (rc)
         return rc;
-    hipLaunchKernelGGL(k_obj_stamp, dim3((n + 255) / 256), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_obj_stamp, dim3((n + 255) / 256), dim3(256), 0, s, d,
+                       static_cast<const uint32_t*>(nullptr), 0u);
+    HIPCHK(hipGetLastError());
+    return RAMCRC_OK;
+}
+
+int ramcrc_assemble_objects_ordered_device(ramcrc_ctx* c, void* d_base, const uint64_t* d_off,
+                                           const uint64_t* d_len, uint32_t* d_out, uint64_t n,
+                                           void* stream)
+{
+    if (n == 0)
+        return c ? RAMCRC_OK : RAMCRC_EINVAL;
+    if (!c || !d_base || !d_off || !d_len)
+        return RAMCRC_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (!d_out) {
+        int rc = grow_device(reinterpret_cast<void**>(&c->obj_out), &c->obj_out_cap, n,
+                             sizeof(uint32_t));
+        if (rc)
+            return rc;
+        d_out = c->obj_out;
+    }
+    int rc = launch_stream(c, static_cast<const uint8_t*>(d_base), d_off, d_len, d_out, n,
+                           RAMCRC_FINALIZE, s, true);
+    if (rc)
+        return rc;
+    BatchDesc d{};
+    d.base = static_cast<const uint8_t*>(d_base);
+    d.off = d_off;
+    d.len = d_len;
+    d.n = n;
+    d.out = d_out;
+    d.flags = RAMCRC_FINALIZE;
+    hipLaunchKernelGGL(k_obj_stamp, dim3((n + 255) / 256), dim3(256), 0, s, d,
+                       static_cast<const uint32_t*>(c->stream_scr + 4 * uint64_t(c->ncu) * kStreamGroups),
+                       c->stream_seq);
     HIPCHK(hipGetLastError());
     return RAMCRC_OK;
 }

@@ -40,7 +40,10 @@
 // from ramcrc_ctx_check.
 
 constexpr uint32_t kStatusOrder = 8u;      // an ORDERED batch was not: nothing written
-constexpr int kStreamWaves = 16;           // waves per workgroup (one workgroup per CU)
+#ifndef RAMCRC_STREAM_WAVES
+#define RAMCRC_STREAM_WAVES 16
+#endif
+constexpr int kStreamWaves = RAMCRC_STREAM_WAVES;   // waves per workgroup (one workgroup per CU)
 constexpr int kStreamGroups = kStreamWaves * 8;   // spans per workgroup
 constexpr int kStreamWin = 8;              // entry slots per lane: 64 entries per group window
 constexpr uint64_t kStreamGap = 4096;      // largest gap between neighbours (page safety)
@@ -65,6 +68,8 @@ struct StreamDesc {
     uint64_t n;
     uint32_t* out;
     uint32_t flags;
+    uint32_t obj;          // kObjects: entry i is bytes [4, len) of the object at off[i]
+                           // (Object::computeChecksum); objects under 24 B are empty
     uint32_t nspan;        // groups of the launch: one span each
     uint32_t seq;          // launch sequence number (refusal word)
     uint32_t* first_ev;    // per span: first entry whose end lies past the span start
@@ -83,11 +88,26 @@ struct StreamGeo {
     uint64_t L;     // span bytes
 };
 
+// [S, E) of entry i.
+__device__ __forceinline__ void stream_range(const StreamDesc& d, uint64_t i, uint64_t& S,
+                                             uint64_t& E)
+{
+    const uint64_t o = reinterpret_cast<uint64_t>(d.base) + d.off[i], L = d.len[i];
+    if (d.obj) {
+        const bool live = L >= kObjHeaderBytes;
+        S = live ? o + 4 : o;
+        E = live ? o + L : o;
+    } else {
+        S = o;
+        E = o + L;
+    }
+}
+
 __device__ __forceinline__ StreamGeo stream_geo(const StreamDesc& d)
 {
-    const uint64_t B = reinterpret_cast<uint64_t>(d.base);
-    const uint64_t R0 = B + d.off[0];
-    const uint64_t R1 = B + d.off[d.n - 1] + d.len[d.n - 1];
+    uint64_t R0, R1, S1;
+    stream_range(d, 0, R0, S1);
+    stream_range(d, d.n - 1, S1, R1);
     StreamGeo g;
     g.A0 = R0 & ~uint64_t(127);
     g.R1 = R1 > g.A0 ? R1 : g.A0;
@@ -117,16 +137,17 @@ __device__ __forceinline__ uint32_t xpow8_any(uint64_t d)
 __global__ __launch_bounds__(256) void k_stream_prep(StreamDesc d)
 {
     const StreamGeo g = stream_geo(d);
-    const uint64_t B = reinterpret_cast<uint64_t>(d.base);
     const uint64_t nsp = (g.ns + g.sps - 1) / g.sps;   // spans holding steps
     bool bad = false;
     for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < d.n;
          i += uint64_t(gridDim.x) * blockDim.x) {
-        const uint64_t S = B + d.off[i], E = S + d.len[i];
+        uint64_t S, E;
+        stream_range(d, i, S, E);
         uint64_t lo = 0;
         bad |= E < S;
         if (i > 0) {
-            const uint64_t Sp = B + d.off[i - 1], Ep = Sp + d.len[i - 1];
+            uint64_t Sp, Ep;
+            stream_range(d, i - 1, Sp, Ep);
             bad |= S < Ep || S - Ep >= kStreamGap || Ep < Sp;
             lo = Ep > g.A0 ? (Ep - g.A0 + g.L - 1) / g.L : 0;
         }
@@ -228,27 +249,30 @@ __global__ __launch_bounds__(kStreamWaves * kWaveSize, 1) void k_stream(StreamDe
     __syncthreads();
     if (refused || wspan * geo.sps >= geo.ns)
         return;   // uniform per wave
-    const uint64_t B = reinterpret_cast<uint64_t>(d.base);
     const uint64_t sg = geo.A0 + span * geo.L;        // this group's span start
     const int32_t Li = int32_t(geo.L);
     const bool finalize = d.flags & RAMCRC_FINALIZE;
 
-    // the wave's 8 spans through one buffer descriptor; bytes past the batch read 0
+    // the wave's 8 spans through one buffer descriptor per step (base advanced
+    // by the step, records shrunk by it): the range check covers voffset + the
+    // immediate, not soffset, so the step offset lives in the descriptor and
+    // every byte past the batch reads 0
     const uint64_t wbase = geo.A0 + wspan * geo.L;
     const uint64_t wlen = geo.R1 > wbase ? min(geo.R1 - wbase, 8 * geo.L) : 0;
-    const uint32_t lo_w = __builtin_amdgcn_readfirstlane(uint32_t(wbase));
-    const uint32_t hi_w = __builtin_amdgcn_readfirstlane(uint32_t(wbase >> 32));
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>((uint64_t(hi_w) << 32) | lo_w), (short)0,
-        int(__builtin_amdgcn_readfirstlane(uint32_t(wlen))), 0x00020000);
     const uint32_t voff = grp * uint32_t(geo.L) + 4 * u;
     auto load_step = [&](uint64_t t) -> u32x4 {
-        const uint32_t so = uint32_t(t) * 128;
+        const uint64_t tb = __builtin_amdgcn_readfirstlane(uint32_t(t)) * uint64_t(128);
+        const uint64_t b = wbase + tb;
+        const uint32_t nrec = wlen > tb ? uint32_t(wlen - tb) : 0u;
+        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<void*>((uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(b >> 32))) << 32) |
+                                    uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(b)))),
+            (short)0, int(__builtin_amdgcn_readfirstlane(nrec)), 0x00020000);
         u32x4 w;
-        w.x = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, so, 0);
-        w.y = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + 32, so, 0);
-        w.z = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + 64, so, 0);
-        w.w = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + 96, so, 0);
+        w.x = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, 0, 0);
+        w.y = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + 32, 0, 0);
+        w.z = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + 64, 0, 0);
+        w.w = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff + 96, 0, 0);
         return w;
     };
 
@@ -278,7 +302,8 @@ __global__ __launch_bounds__(kStreamWaves * kWaveSize, 1) void k_stream(StreamDe
         for (int m = 0; m < kStreamWin; m++) {
             const uint64_t e = e0 + u + 8 * uint64_t(m);
             if (e < d.n) {
-                const uint64_t S = B + d.off[e], E = S + d.len[e];
+                uint64_t S, E;
+                stream_range(d, e, S, E);
                 Sr[m] = rel(S);
                 Er[m] = rel(E);
             } else {
@@ -289,6 +314,11 @@ __global__ __launch_bounds__(kStreamWaves * kWaveSize, 1) void k_stream(StreamDe
         cnt = 0;
     };
     load_window();
+    // empty entries exactly at the start of step 0 belong to no span's boundaries
+    // (a span owns (start, start + L]): span 0 writes them
+    if (span == 0)
+        for (uint64_t i = u; i < e0; i += 8)
+            d.out[i] = finalize ? 0u : 0xFFFFFFFFu;
     // the group's first entry may have started before the span: its start is done
     bool Sd = u == 0 && Sr[0] <= 0, Ed = false;
     bool cross = u == 0 && Sr[0] < 0;   // started in an earlier span: k_stream_fix finishes it
@@ -296,6 +326,7 @@ __global__ __launch_bounds__(kStreamWaves * kWaveSize, 1) void k_stream(StreamDe
     // state at the end of the previous step: an entry starting exactly at the
     // span start gets its initial state injected into the first four bytes
     uint32_t G = grp_or(u == 0 && Sr[0] == 0 ? 1u : 0u) ? 0xFFFFFFFFu : 0u;
+    bool overrun = false;
 
     u32x4 buf[kStreamU];
 #pragma unroll
@@ -331,8 +362,7 @@ __global__ __launch_bounds__(kStreamWaves * kWaveSize, 1) void k_stream(StreamDe
             uint32_t guard = 0;
             while (true) {
                 if (++guard > kStreamMaxPass) {   // cannot happen; never spin the GPU
-                    if (lane == 0)
-                        atomicOr(d.status, kStatusSticky | kStatusBins);
+                    overrun = true;
                     break;
                 }
                 int32_t nb = !Sd ? Sr[0] : (!Ed ? Er[0] : kBig);
@@ -431,6 +461,8 @@ __global__ __launch_bounds__(kStreamWaves * kWaveSize, 1) void k_stream(StreamDe
     }
     // span end: the state (of an entry still open, or of the whole span) and the
     // cross-span marker (lane 0 owns the group's first entry)
+    if (overrun)   // refuse: RAMCRC_EINTERNAL from ramcrc_ctx_check
+        atomicOr(d.status, kStatusSticky | kStatusBins);
     if (u == 0) {
         d.span_t[span] = G;
         if (!xe_done)
@@ -452,10 +484,12 @@ __global__ __launch_bounds__(256) void k_stream_fix(StreamDesc d)
     const uint32_t i = d.xe_idx[g];
     if (i == kNoIdx)
         return;
-    const uint64_t B = reinterpret_cast<uint64_t>(d.base);
-    const uint64_t S = B + d.off[i], E = S + d.len[i];
+    uint64_t S, E;
+    stream_range(d, i, S, E);
     const uint64_t sg = geo.A0 + g * geo.L;
-    const uint64_t h = (S - 1 - geo.A0) / geo.L;   // the span whose boundaries held S
+    // the span holding S: its group re-based there (an entry starting exactly at
+    // a span start had its initial state injected by that span's group)
+    const uint64_t h = (S - geo.A0) / geo.L;
     uint32_t st = d.span_t[h];
     if (h + 1 < g) {
         const uint32_t cL = xpow8_any(geo.L);

@@ -86,6 +86,7 @@ def lib():
         "ramcrc_segment_fill_objects": (i32, [vp, u32, u32, u64, _c.POINTER(u32), vp]),
         "ramcrc_assemble_objects_device": (i32, [vp, vp, vp, vp, vp, u64, vp]),
         "ramcrc_assemble_objects_host": (i32, [vp, vp, vp, u64]),
+        "ramcrc_assemble_objects_ordered_device": (i32, [vp, vp, vp, vp, vp, u64, vp]),
         "ramcrc_ctx_set_timing": (i32, [vp, i32]),
         "ramcrc_ctx_scan_time": (i32, [vp, _c.POINTER(_c.c_double), _c.POINTER(u64)]),
         "ramcrc_ctx_status": (i32, [vp, _c.POINTER(u32)]),
@@ -380,14 +381,17 @@ class Context:
         _check(rc, "ramcrc_segment_fill_objects_device")
         return per.value, int(cert[0]), int(cert[1])
 
-    def assemble_objects(self, data, off, length, out=None, stream=None):
+    def assemble_objects(self, data, off, length, out=None, stream=None, ordered=False):
         """Object::assembleForLog's checksum for serialized objects in `data`
         (uint8 CUDA tensor, modified in place): header.checksum of object i
-        (bytes [off[i], off[i]+4)) = Crc32C over bytes [4, length[i])."""
+        (bytes [off[i], off[i]+4)) = Crc32C over bytes [4, length[i]).
+        ordered=True: the objects lie in log order (one stream pass)."""
         n = off.numel()
-        rc = lib().ramcrc_assemble_objects_device(self._h, _ptr(data), _ptr(off), _ptr(length),
-                                                  _ptr(out), n, _stream(stream))
-        _check(rc, "ramcrc_assemble_objects_device")
+        fn = (lib().ramcrc_assemble_objects_ordered_device if ordered
+              else lib().ramcrc_assemble_objects_device)
+        rc = fn(self._h, _ptr(data), _ptr(off), _ptr(length), _ptr(out), n, _stream(stream))
+        _check(rc, "ramcrc_assemble_objects_ordered_device" if ordered
+               else "ramcrc_assemble_objects_device")
         return out
 
     def assemble_objects_host(self, objects):
