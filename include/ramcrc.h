@@ -276,6 +276,22 @@ int ramcrc_verify_objects_device(ramcrc_ctx* ctx, const void* d_base, uint64_t s
                                  const uint64_t* d_n_entries, uint32_t* d_obj_crc,
                                  ramcrc_seg_status* d_status, void* stream);
 
+/* The same checks with the objects checksummed in one ordered pass over each
+ * segment's bytes (the RAMCRC_ORDERED stream, spans per segment) instead of
+ * object by object: every object's Object::computeChecksum and its
+ * comparison with the stored checksum happen as the pass crosses the object's
+ * end.  n_seg is the number of segments the walk covered.  The record table
+ * must be the one ramcrc_segment_walk_device wrote: each segment's records
+ * contiguous and in offset order (both walkers write them so); a table that
+ * is not is refused (nothing checked, RAMCRC_EORDER from ramcrc_ctx_check)
+ * and can be verified with ramcrc_verify_objects_device.  Results are
+ * identical to ramcrc_verify_objects_device's. */
+int ramcrc_verify_objects_ordered_device(ramcrc_ctx* ctx, const void* d_base, uint64_t seg_stride,
+                                         uint64_t n_seg, const ramcrc_seg_entry* d_entries,
+                                         uint64_t entries_cap, const uint64_t* d_n_entries,
+                                         uint32_t* d_obj_crc, ramcrc_seg_status* d_status,
+                                         void* stream);
+
 /* Host append path (src/Segment.cc:197-228 with src/Object.cc:213-218):
  * appends LOG_ENTRY_TYPE_OBJ entries holding objects {tableId 0, key = 8-byte
  * counter from first_key, version 0, timestamp 0, value_len value bytes} to an

@@ -2474,6 +2474,9 @@ struct ramcrc_ctx {
     uint32_t* stream_scr = nullptr;
     uint64_t stream_scr_cap = 0;
     uint32_t stream_seq = 0;
+    uint32_t* stream_bad = nullptr;   // the refusal word of ordered launches (own allocation)
+    unsigned long long* rec_first = nullptr;   // records mode: seq << 32 | first record, per segment
+    uint64_t rec_first_cap = 0;
     // benchmark timing of the scan kernels
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_used, ev_free;
@@ -2717,6 +2720,31 @@ int launch_planned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s)
     return bin_finish<kMode>(c, d, s, 1, so);
 }
 
+// Scratch of the ordered launches.  The refusal word has an allocation of its
+// own and the sequence number only grows, so no word an earlier launch left
+// (of any layout) can read as this launch's refusal or segment index.
+int reserve_stream(ramcrc_ctx* c, uint64_t words)
+{
+    if (!c->stream_bad) {
+        if (hipMalloc(reinterpret_cast<void**>(&c->stream_bad), 16) != hipSuccess) {
+            c->stream_bad = nullptr;
+            return RAMCRC_ENOMEM;
+        }
+        HIPCHK(hipMemset(c->stream_bad, 0, 16));
+    }
+    if (c->stream_scr_cap < words)
+        return grow_device(reinterpret_cast<void**>(&c->stream_scr), &c->stream_scr_cap, words,
+                           sizeof(uint32_t));
+    return RAMCRC_OK;
+}
+
+uint32_t next_stream_seq(ramcrc_ctx* c)
+{
+    if (++c->stream_seq == 0)
+        ++c->stream_seq;   // 0 is the word's initial value
+    return c->stream_seq;
+}
+
 // Ordered batch (RAMCRC_ORDERED): k_stream_prep -> k_stream -> k_stream_fix
 // (stream.h).  Every launch gets a new sequence number, so a refusal word
 // left by an earlier launch never stops a later one.
@@ -2726,15 +2754,9 @@ int launch_stream(ramcrc_ctx* c, const uint8_t* base, const uint64_t* off, const
     if (n >= (1ull << 32) - 1)
         return RAMCRC_EINVAL;   // 32-bit entry indices
     const uint32_t nspan = uint32_t(c->ncu) * kStreamGroups;
-    const uint64_t words = 4ull * nspan + 4;
-    if (c->stream_scr_cap < words) {
-        int rc = grow_device(reinterpret_cast<void**>(&c->stream_scr), &c->stream_scr_cap, words,
-                             sizeof(uint32_t));
-        if (rc)
-            return rc;
-        HIPCHK(hipMemset(c->stream_scr, 0, c->stream_scr_cap * sizeof(uint32_t)));
-        c->stream_seq = 0;
-    }
+    int rc = reserve_stream(c, 4ull * nspan);
+    if (rc)
+        return rc;
     StreamDesc d{};
     d.base = base;
     d.off = off;
@@ -2744,12 +2766,12 @@ int launch_stream(ramcrc_ctx* c, const uint8_t* base, const uint64_t* off, const
     d.flags = flags;
     d.obj = objects ? 1u : 0u;
     d.nspan = nspan;
-    d.seq = ++c->stream_seq == 0 ? ++c->stream_seq : c->stream_seq;   // never 0 (the initial word)
+    d.seq = next_stream_seq(c);
     d.first_ev = c->stream_scr;
     d.span_t = c->stream_scr + nspan;
     d.xe_val = c->stream_scr + 2 * uint64_t(nspan);
     d.xe_idx = c->stream_scr + 3 * uint64_t(nspan);
-    d.bad_seq = c->stream_scr + 4 * uint64_t(nspan);
+    d.bad_seq = c->stream_bad;
     d.status = c->status;
     uint64_t pg = (n + 255) / 256;
     if (pg > uint64_t(c->ncu) * 8)
@@ -2758,10 +2780,75 @@ int launch_stream(ramcrc_ctx* c, const uint8_t* base, const uint64_t* off, const
     HIPCHK(hipGetLastError());
     {
         ScanTimer t(c, s);
-        t.launch(k_stream, dim3(c->ncu), dim3(kStreamWaves * kWaveSize), d);
+        t.launch(k_stream<false>, dim3(c->ncu), dim3(kStreamWaves * kWaveSize), d);
     }
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_stream_fix, dim3((nspan + 255) / 256), dim3(256), 0, s, d);
+    hipLaunchKernelGGL(k_stream_fix<false>, dim3((nspan + 255) / 256), dim3(256), 0, s, d);
+    HIPCHK(hipGetLastError());
+    return RAMCRC_OK;
+}
+
+// Records mode (ramcrc_verify_objects_device): the objects of a walk's record
+// table, segment by segment.  spr spans per segment (a multiple of 8) so that
+// about one span per group of a full grid; more segments than that run as
+// more workgroups.
+int launch_stream_records(ramcrc_ctx* c, const BatchDesc& bd, uint64_t nseg, hipStream_t s)
+{
+    if (bd.n >= (1ull << 32) - 1 || nseg >= (1ull << 32))
+        return RAMCRC_EINVAL;
+    const uint64_t full = uint64_t(c->ncu) * kStreamGroups;
+    uint64_t spr = full / (nseg ? nseg : 1) / 8 * 8;
+    if (spr < 8)
+        spr = 8;
+    if (spr > 4096)
+        spr = 4096;
+    const uint64_t nspan = nseg * spr;
+    int rc = reserve_stream(c, 4 * nspan);
+    if (rc)
+        return rc;
+    if (c->rec_first_cap < nseg) {
+        rc = grow_device(reinterpret_cast<void**>(&c->rec_first), &c->rec_first_cap, nseg,
+                         sizeof(unsigned long long));
+        if (rc)
+            return rc;
+        HIPCHK(hipMemset(c->rec_first, 0, c->rec_first_cap * sizeof(unsigned long long)));
+    }
+    StreamDesc d{};
+    d.base = bd.base;
+    d.n = bd.n;
+    d.out = bd.out;
+    d.flags = RAMCRC_FINALIZE;
+    d.nspan = uint32_t(nspan);
+    d.seq = next_stream_seq(c);
+    d.first_ev = c->stream_scr;
+    d.span_t = c->stream_scr + nspan;
+    d.xe_val = c->stream_scr + 2 * nspan;
+    d.xe_idx = c->stream_scr + 3 * nspan;
+    d.bad_seq = c->stream_bad;
+    d.seg_first = c->rec_first;
+    d.status = c->status;
+    d.rec = bd.rec;
+    d.n_dev = bd.n_dev;
+    d.vstat = bd.vstat;
+    d.stride = bd.seg_bytes;
+    d.nseg = nseg;
+    d.spr = uint32_t(spr);
+    uint64_t pg = (bd.n + 255) / 256;
+    if (pg > uint64_t(c->ncu) * 8)
+        pg = uint64_t(c->ncu) * 8;
+    if (pg == 0)
+        pg = 1;
+    hipLaunchKernelGGL(k_stream_rprep, dim3(pg), dim3(256), 0, s, d);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_stream_rprep2, dim3(pg), dim3(256), 0, s, d);
+    HIPCHK(hipGetLastError());
+    {
+        ScanTimer t(c, s);
+        t.launch(k_stream<true>, dim3(nspan / kStreamGroups + (nspan % kStreamGroups ? 1 : 0)),
+                 dim3(kStreamWaves * kWaveSize), d);
+    }
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_stream_fix<true>, dim3((nspan + 255) / 256), dim3(256), 0, s, d);
     HIPCHK(hipGetLastError());
     return RAMCRC_OK;
 }
@@ -2801,6 +2888,7 @@ struct WalkDesc {
     uint64_t cap;
     unsigned long long* n_entries;
     const uint32_t* only;   // nullable: walk only the segments with only[seg] != 0
+    uint64_t* seg_base;     // nullable: per segment, the first slot of its records
 };
 
 // CRC32C update by the m (1..4) bytes in the low end of v; t[j][b] = X^(j+1)(b).
@@ -2856,6 +2944,12 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
             continue;   // walked by the parallel walk (uniform per workgroup)
         const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
         const ramcrc_seg_cert cert = w.certs[seg];
+        // Two passes: the first counts the records, one atomic allocates them,
+        // the second writes them -- so every segment's records are contiguous
+        // and in offset order (the parallel walk's are too), which the ordered
+        // object scan relies on (stream.h, records mode).
+        unsigned long long rbase = 0, rdone = 0, rtotal = 0;
+        for (int pass = 0; pass < 2; pass++) {
         uint32_t pos = 0, crc = 0xFFFFFFFFu, count = 0, flags = 0;
         // Parked entries: lane j holds entry j of the current batch of 64 --
         // its offset and the 4 bytes from its header on.  Its length is
@@ -2896,15 +2990,13 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
             for (int s = 1; s < kWaveSize; s <<= 1)
                 c ^= __shfl_xor(c, s, kWaveSize);
             crc = mulmod_horner(crc, xm[total]) ^ c;
-            if (nrec) {
-                unsigned long long b = 0;
-                if (lane == 0)
-                    b = atomicAdd(w.n_entries, (unsigned long long)nrec);
-                b = __shfl(b, 0, kWaveSize);
+            if (nrec && pass == 0) {
+                rtotal += nrec;
+            } else if (nrec) {
+                const unsigned long long b = rbase + rdone;
                 if (lane < int(nrec) && b + lane < w.cap)
                     w.entries[b + lane] = u32x4{uint32_t(seg), rpos, rlen, rinfo};
-                if (b + nrec > w.cap)
-                    flags |= RAMCRC_SEG_TABLE_FULL;
+                rdone += nrec;
             }
             ns = 0;
         };
@@ -3004,6 +3096,20 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
         count = steps - (overrun ? 1u : 0u);
         if (ns)
             flush(overrun ? ns - 1 : ns, tail);
+        if (pass == 0) {
+            unsigned long long b = 0;
+            if (lane == 0 && rtotal)
+                b = atomicAdd(w.n_entries, rtotal);
+            rbase = __shfl(b, 0, kWaveSize);
+            if (lane == 0 && w.seg_base)
+                w.seg_base[seg] = rbase;
+            if (rtotal == 0)
+                pass = 1;   // nothing to write: the second pass is this one
+        }
+        if (rbase + rtotal > w.cap)
+            flags |= RAMCRC_SEG_TABLE_FULL;
+        if (pass == 0)
+            continue;
         const uint32_t fin = ~crc_small(tab, crc, cert.segment_length, 4);
         if (!(flags & (RAMCRC_SEG_PAST_CAPACITY | RAMCRC_SEG_CYCLE))) {
             if (pos > cert.segment_length)
@@ -3021,6 +3127,7 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
             st.bad_objects = 0;
             w.status[seg] = st;
         }
+        }   // pass
     }
 }
 
@@ -4301,10 +4408,15 @@ __device__ __forceinline__ uint32_t replay_header_bytes(uint32_t type)
     }
 }
 
-__global__ __launch_bounds__(256) void k_obj_compare(BatchDesc d, ramcrc_seg_status* status)
+// skip_objs: every readable object was checked by the ordered scan
+// (k_stream<true>); bad_seq (nullable) == seq: that scan was refused, and
+// nothing is checked here either.
+__global__ __launch_bounds__(256) void k_obj_compare(BatchDesc d, ramcrc_seg_status* status,
+                                                     int skip_objs, const uint32_t* bad_seq,
+                                                     uint32_t seq)
 {
     const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= entry_count<kRecords>(d))
+    if (i >= entry_count<kRecords>(d) || (bad_seq && *bad_seq == seq))
         return;
     const u32x4 r = d.rec[i];
     const uint32_t type = r.w & 0x3f;
@@ -4312,8 +4424,9 @@ __global__ __launch_bounds__(256) void k_obj_compare(BatchDesc d, ramcrc_seg_sta
     if (hdr == 0)
         return;
     const bool readable = r.z >= hdr && !(r.w & kRecOverlong);
-    if (d.vstat && type == RAMCRC_LOG_ENTRY_TYPE_OBJ && readable && !is_large(uint64_t(r.z) - 4))
-        return;   // compared by k_entries beside its scan (objects below the 64 KiB split)
+    if (d.vstat && type == RAMCRC_LOG_ENTRY_TYPE_OBJ && readable &&
+        (skip_objs || !is_large(uint64_t(r.z) - 4)))
+        return;   // compared beside the scan (k_stream: all; k_entries: below the 64 KiB split)
     const uint64_t payload = reinterpret_cast<uint64_t>(d.base) + uint64_t(r.x) * d.seg_bytes +
                              r.y + 1 + ((r.w >> 6) & 3) + 1;
     const gu8* p = reinterpret_cast<const gu8*>(payload);
@@ -4548,6 +4661,8 @@ int ramcrc_ctx_destroy(ramcrc_ctx* c)
     if (c->walk_blocks) (void)hipFree(c->walk_blocks);
     if (c->walk_pool_used) (void)hipFree(c->walk_pool_used);
     if (c->stream_scr) (void)hipFree(c->stream_scr);
+    if (c->stream_bad) (void)hipFree(c->stream_bad);
+    if (c->rec_first) (void)hipFree(c->rec_first);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -5011,6 +5126,13 @@ int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_s
     w.cap = entries_cap;
     w.n_entries = reinterpret_cast<unsigned long long*>(d_n_entries);
     w.only = nullptr;
+    {
+        int rc0 = grow_device(reinterpret_cast<void**>(&c->walk_base), &c->walk_base_cap, n_seg,
+                              sizeof(uint64_t));
+        if (rc0)
+            return rc0;
+    }
+    w.seg_base = c->walk_base;   // every segment's first record slot (both walkers)
     uint64_t grid = n_seg;
     if (grid > uint64_t(64) * c->ncu)
         grid = uint64_t(64) * c->ncu;
@@ -5028,9 +5150,6 @@ int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_s
         if (!rc)
             rc = grow_device(reinterpret_cast<void**>(&c->walk_fallback), &c->walk_fallback_cap,
                              n_seg, sizeof(uint32_t));
-        if (!rc)
-            rc = grow_device(reinterpret_cast<void**>(&c->walk_base), &c->walk_base_cap, n_seg,
-                             sizeof(uint64_t));
         if (!rc)
             rc = grow_device(&c->walk_recs, &c->walk_recs_cap, total * kPartRec, sizeof(uint2));
         // the pool holds A's records past each part's first block: sized for
@@ -5167,7 +5286,46 @@ int ramcrc_verify_objects_device(ramcrc_ctx* c, const void* d_base, uint64_t seg
     if (rc)
         return rc;
     const uint64_t grid = (entries_cap + 255) / 256;
-    hipLaunchKernelGGL(k_obj_compare, dim3(grid), dim3(256), 0, s, d, d_status);
+    hipLaunchKernelGGL(k_obj_compare, dim3(grid), dim3(256), 0, s, d, d_status, 0,
+                       static_cast<const uint32_t*>(nullptr), 0u);
+    HIPCHK(hipGetLastError());
+    return RAMCRC_OK;
+}
+
+int ramcrc_verify_objects_ordered_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride,
+                                         uint64_t n_seg, const ramcrc_seg_entry* d_entries,
+                                         uint64_t entries_cap, const uint64_t* d_n_entries,
+                                         uint32_t* d_obj_crc, ramcrc_seg_status* d_status,
+                                         void* stream)
+{
+    if (!c)
+        return RAMCRC_EINVAL;
+    if (entries_cap == 0 || n_seg == 0)
+        return RAMCRC_OK;
+    if (!d_base || !d_entries || !d_n_entries || !d_obj_crc || !d_status || (seg_stride & 15) ||
+        (reinterpret_cast<uintptr_t>(d_base) & 15))
+        return RAMCRC_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    BatchDesc d{};
+    d.base = static_cast<const uint8_t*>(d_base);
+    d.seg_bytes = seg_stride;
+    d.n = entries_cap;
+    d.vstat = d_status;
+    d.rec = reinterpret_cast<const u32x4*>(d_entries);
+    d.n_dev = d_n_entries;
+    d.seg_status = reinterpret_cast<const u32x4*>(d_status);
+    d.out = d_obj_crc;
+    d.flags = RAMCRC_FINALIZE;
+    int rc = launch_stream_records(c, d, n_seg, s);
+    if (rc)
+        return rc;
+    // the other replayed types (and nothing when the scan was refused: the
+    // compare would read object CRCs that were never written)
+    const uint64_t grid = (entries_cap + 255) / 256;
+    hipLaunchKernelGGL(k_obj_compare, dim3(grid), dim3(256), 0, s, d, d_status, 1,
+                       static_cast<const uint32_t*>(c->stream_bad), c->stream_seq);
     HIPCHK(hipGetLastError());
     return RAMCRC_OK;
 }
@@ -5240,8 +5398,7 @@ int ramcrc_assemble_objects_ordered_device(ramcrc_ctx* c, void* d_base, const ui
     d.out = d_out;
     d.flags = RAMCRC_FINALIZE;
     hipLaunchKernelGGL(k_obj_stamp, dim3((n + 255) / 256), dim3(256), 0, s, d,
-                       static_cast<const uint32_t*>(c->stream_scr + 4 * uint64_t(c->ncu) * kStreamGroups),
-                       c->stream_seq);
+                       static_cast<const uint32_t*>(c->stream_bad), c->stream_seq);
     HIPCHK(hipGetLastError());
     return RAMCRC_OK;
 }

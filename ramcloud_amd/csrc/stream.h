@@ -78,7 +78,60 @@ struct StreamDesc {
     uint32_t* xe_idx;      // per span: that entry, or kNoIdx
     uint32_t* bad_seq;     // == seq: this launch's batch was refused by k_stream_prep
     uint32_t* status;
+    // records mode (k_stream<true>): the object records of a segment walk
+    const u32x4* rec;      // ramcrc_seg_entry {segment, offset, length, header}
+    const uint64_t* n_dev; // live records (device), <= n
+    ramcrc_seg_status* vstat;   // the walk's status per segment; bad_objects counted here
+    uint64_t stride;       // segment i at base + i * stride
+    uint64_t nseg;
+    uint32_t spr;          // spans per segment (a multiple of 8: a wave stays in one segment)
+    unsigned long long* seg_first;   // per segment: seq << 32 | its first record (k_stream_rprep)
 };
+
+// One segment of a records-mode launch: its records are rec[first, first +
+// count), contiguous and in offset order (both walkers write them so), and its
+// stream covers [0, rlen) -- the end of its last entry -- cut into spr spans
+// of L bytes.  ok: the walk passed it (RAMCRC_SEG_OK) and this launch indexed it.
+struct SegInfo {
+    bool ok;
+    uint64_t first, count, rlen, L, sps, addr;
+};
+
+// Object bytes of a walk record relative to its segment: [S, E) of
+// Object::computeChecksum (payload bytes [4, length)), or an empty range at
+// the payload for records that are not checked here (other types, objects
+// shorter than their header or running past the segment).
+__device__ __forceinline__ bool rec_range(const u32x4& r, uint64_t& S, uint64_t& E)
+{
+    const uint64_t payload = uint64_t(r.y) + 1 + ((r.w >> 6) & 3) + 1;
+    const bool obj = (r.w & (0x3f | kRecOverlong)) == RAMCRC_LOG_ENTRY_TYPE_OBJ &&
+                     r.z >= kObjHeaderBytes;
+    S = obj ? payload + 4 : payload;
+    E = obj ? payload + r.z : payload;
+    return obj;
+}
+
+__device__ __forceinline__ SegInfo seg_info(const StreamDesc& d, uint64_t s)
+{
+    SegInfo g{};
+    const u32x4 st = *reinterpret_cast<const u32x4*>(&d.vstat[s]);   // flags, checksum, entries
+    const unsigned long long f = d.seg_first[s];
+    g.count = st.z;
+    g.first = uint32_t(f);
+    g.ok = (st.x & RAMCRC_SEG_OK) && g.count > 0 && uint32_t(f >> 32) == d.seq;
+    if (!g.ok)
+        return g;
+    uint64_t S, E;
+    rec_range(d.rec[g.first + g.count - 1], S, E);
+    g.rlen = E;
+    const uint64_t steps = (g.rlen + 127) / 128;
+    g.sps = (steps + d.spr - 1) / d.spr;
+    if (g.sps == 0)
+        g.sps = 1;
+    g.L = 128 * g.sps;
+    g.addr = reinterpret_cast<uint64_t>(d.base) + s * d.stride;
+    return g;
+}
 
 struct StreamGeo {
     uint64_t A0;    // start of step 0: the first entry's 128-byte line
@@ -165,6 +218,85 @@ __global__ __launch_bounds__(256) void k_stream_prep(StreamDesc d)
     }
 }
 
+// Records mode, pass 1: every segment's first record, tagged with the launch
+// sequence number.  A segment whose records form two runs, or whose offsets do
+// not increase, is refused (it cannot come from the walk).
+__global__ __launch_bounds__(256) void k_stream_rprep(StreamDesc d)
+{
+    const uint64_t live = *d.n_dev < d.n ? *d.n_dev : d.n;
+    bool bad = false;
+    for (uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; r < live;
+         r += uint64_t(gridDim.x) * blockDim.x) {
+        const u32x4 x = d.rec[r];
+        if (x.x >= d.nseg) {
+            bad = true;
+            continue;
+        }
+        // only segments that passed the walk are checked (the records of a
+        // failed one -- e.g. an offset wrap walked backwards -- are skipped)
+        if (!(reinterpret_cast<const u32x4*>(d.vstat)[x.x].x & RAMCRC_SEG_OK))
+            continue;
+        const u32x4 y = r ? d.rec[r - 1] : u32x4{0xFFFFFFFFu, 0u, 0u, 0u};
+        if (y.x != x.x) {
+            const unsigned long long old =
+                atomicExch(&d.seg_first[x.x], (static_cast<unsigned long long>(d.seq) << 32) | r);
+            bad |= uint32_t(old >> 32) == d.seq;   // a second run of the segment
+        } else {
+            bad |= y.y >= x.y;
+        }
+    }
+    if (bad) {
+        *d.bad_seq = d.seq;
+        atomicOr(d.status, kStatusSticky | kStatusOrder);
+    }
+}
+
+// Records mode, pass 2: the first record of every span (as k_stream_prep,
+// per segment).
+__global__ __launch_bounds__(256) void k_stream_rprep2(StreamDesc d)
+{
+    if (*d.bad_seq == d.seq)
+        return;
+    const uint64_t live = *d.n_dev < d.n ? *d.n_dev : d.n;
+    bool bad = false;
+    for (uint64_t r = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; r < live;
+         r += uint64_t(gridDim.x) * blockDim.x) {
+        const u32x4 x = d.rec[r];
+        const SegInfo g = seg_info(d, x.x);
+        if (!g.ok)
+            continue;
+        if (r < g.first || r >= g.first + g.count) {
+            bad = true;   // the table does not hold exactly the segment's walked entries
+            continue;
+        }
+        uint64_t S, E, lo = 0;
+        rec_range(x, S, E);
+        if (r > g.first) {
+            uint64_t Sp, Ep;
+            rec_range(d.rec[r - 1], Sp, Ep);
+            bad |= S < Ep;
+            lo = (Ep + g.L - 1) / g.L;
+        }
+        uint64_t hi = (E + g.L - 1) / g.L;
+        const bool last = r == g.first + g.count - 1;
+        if (last || hi > d.spr)
+            hi = d.spr;
+        for (uint64_t k = lo; k < hi; k++)
+            d.first_ev[uint64_t(x.x) * d.spr + k] =
+                (last && k * g.L >= E) ? uint32_t(g.first + g.count) : uint32_t(r);
+    }
+    // a segment that passed the walk but has no records in this table
+    for (uint64_t sg = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; sg < d.nseg;
+         sg += uint64_t(gridDim.x) * blockDim.x) {
+        const u32x4 st = *reinterpret_cast<const u32x4*>(&d.vstat[sg]);
+        bad |= (st.x & RAMCRC_SEG_OK) && st.z > 0 && uint32_t(d.seg_first[sg] >> 32) != d.seq;
+    }
+    if (bad) {
+        *d.bad_seq = d.seq;
+        atomicOr(d.status, kStatusSticky | kStatusOrder);
+    }
+}
+
 // XOR / min over the 8 lanes of a group: quad swaps, then the half-row mirror.
 __device__ __forceinline__ uint32_t grp_xor(uint32_t v)
 {
@@ -235,6 +367,10 @@ __device__ __forceinline__ void stream_fill(uint8_t* lds)
     }
 }
 
+// One span per group of 8 lanes.  kRec: records mode (object checks of a
+// segment walk; spans per segment, the stored Object::Header::checksum compared
+// at each object's end).
+template <bool kRec>
 __global__ __launch_bounds__(kStreamWaves * kWaveSize, 1) void k_stream(StreamDesc d)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsStream];
@@ -244,22 +380,54 @@ __global__ __launch_bounds__(kStreamWaves * kWaveSize, 1) void k_stream(StreamDe
     const uint64_t wspan = (uint64_t(blockIdx.x) * kStreamWaves + wave) * 8;   // first span of the wave
     const uint64_t span = wspan + grp;
     const bool refused = *d.bad_seq == d.seq;
-    const StreamGeo geo = stream_geo(d);
+    // geometry: this group's span [sg, sg + L), the wave's bytes [wbase, wbase + wlen),
+    // entries [e_lo, e_hi)
+    uint64_t sg, L, sps, wbase, wlen, e0, e_hi, seg = 0;
+    bool idle_wave, idle;
+    if (kRec) {
+        seg = wspan / d.spr;   // uniform: the wave's 8 spans are in one segment
+        const SegInfo gi = seg < d.nseg ? seg_info(d, seg) : SegInfo{};
+        const uint64_t k = span - seg * d.spr, k0 = wspan - seg * d.spr;
+        idle_wave = refused || !gi.ok;
+        L = gi.L;
+        sps = gi.sps;
+        sg = gi.addr + k * L;
+        wbase = gi.addr + k0 * L;
+        // whole dwords: a dword load partly past the limit would read as 0
+        const uint64_t rl4 = (gi.rlen + 3) & ~uint64_t(3);
+        wlen = rl4 > k0 * L ? min(rl4 - k0 * L, 8 * L) : 0;
+        idle = idle_wave;
+        e_hi = gi.first + gi.count;
+        e0 = idle ? e_hi : d.first_ev[span];
+    } else {
+        const StreamGeo geo = stream_geo(d);
+        idle_wave = refused || wspan * geo.sps >= geo.ns;
+        L = geo.L;
+        sps = geo.sps;
+        sg = geo.A0 + span * L;
+        wbase = geo.A0 + wspan * L;
+        // whole dwords (the last one may pass R1 by up to 3 bytes, inside its
+        // page): a dword load partly past the limit would read as 0
+        const uint64_t r4 = (geo.R1 + 3) & ~uint64_t(3);
+        wlen = r4 > wbase ? min(r4 - wbase, 8 * L) : 0;
+        idle = span * geo.sps >= geo.ns;
+        e_hi = d.n;
+        e0 = idle ? d.n : 0;
+    }
     stream_fill(lds);
+    if (!kRec && !idle_wave && !idle)
+        e0 = d.first_ev[span];
     __syncthreads();
-    if (refused || wspan * geo.sps >= geo.ns)
+    if (__builtin_amdgcn_readfirstlane(idle_wave ? 1 : 0))
         return;   // uniform per wave
-    const uint64_t sg = geo.A0 + span * geo.L;        // this group's span start
-    const int32_t Li = int32_t(geo.L);
+    const int32_t Li = int32_t(L);
     const bool finalize = d.flags & RAMCRC_FINALIZE;
 
     // the wave's 8 spans through one buffer descriptor per step (base advanced
     // by the step, records shrunk by it): the range check covers voffset + the
     // immediate, not soffset, so the step offset lives in the descriptor and
     // every byte past the batch reads 0
-    const uint64_t wbase = geo.A0 + wspan * geo.L;
-    const uint64_t wlen = geo.R1 > wbase ? min(geo.R1 - wbase, 8 * geo.L) : 0;
-    const uint32_t voff = grp * uint32_t(geo.L) + 4 * u;
+    const uint32_t voff = grp * uint32_t(L) + 4 * u;
     auto load_step = [&](uint64_t t) -> u32x4 {
         const uint64_t tb = __builtin_amdgcn_readfirstlane(uint32_t(t)) * uint64_t(128);
         const uint64_t b = wbase + tb;
@@ -289,8 +457,6 @@ __global__ __launch_bounds__(kStreamWaves * kWaveSize, 1) void k_stream(StreamDe
     };
 
     // entry window: lane u holds entries e0 + u + 8 m, m = 0..7, relative to the span start
-    const bool idle = span * geo.sps >= geo.ns;
-    uint64_t e0 = idle ? d.n : d.first_ev[span];
     int32_t Sr[kStreamWin], Er[kStreamWin];
     uint32_t cnt = 0;   // slots this lane has finished
     auto rel = [&](uint64_t x) -> int32_t {
@@ -301,9 +467,16 @@ __global__ __launch_bounds__(kStreamWaves * kWaveSize, 1) void k_stream(StreamDe
 #pragma unroll
         for (int m = 0; m < kStreamWin; m++) {
             const uint64_t e = e0 + u + 8 * uint64_t(m);
-            if (e < d.n) {
+            if (e < e_hi) {
                 uint64_t S, E;
-                stream_range(d, e, S, E);
+                if (kRec) {
+                    rec_range(d.rec[e], S, E);
+                    const uint64_t a = sg - (span - seg * d.spr) * L;   // the segment's address
+                    S += a;
+                    E += a;
+                } else {
+                    stream_range(d, e, S, E);
+                }
                 Sr[m] = rel(S);
                 Er[m] = rel(E);
             } else {
@@ -315,8 +488,9 @@ __global__ __launch_bounds__(kStreamWaves * kWaveSize, 1) void k_stream(StreamDe
     };
     load_window();
     // empty entries exactly at the start of step 0 belong to no span's boundaries
-    // (a span owns (start, start + L]): span 0 writes them
-    if (span == 0)
+    // (a span owns (start, start + L]): span 0 writes them (no record mode entry
+    // starts at a segment's offset 0)
+    if (!kRec && span == 0)
         for (uint64_t i = u; i < e0; i += 8)
             d.out[i] = finalize ? 0u : 0xFFFFFFFFu;
     // the group's first entry may have started before the span: its start is done
@@ -327,21 +501,33 @@ __global__ __launch_bounds__(kStreamWaves * kWaveSize, 1) void k_stream(StreamDe
     // span start gets its initial state injected into the first four bytes
     uint32_t G = grp_or(u == 0 && Sr[0] == 0 ? 1u : 0u) ? 0xFFFFFFFFu : 0u;
     bool overrun = false;
+    uint32_t stored = 0;   // records mode: Object::Header::checksum of this lane's open object
+    // records mode: the previous step's dword 24 + u (lane 7: step bytes 124..127);
+    // before step 0 the bytes ahead of the span (none ahead of a segment's first span)
+    uint32_t prev3 = 0;
+    if (kRec && span != seg * d.spr)
+        prev3 = *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(sg - 32 + 4 * u);
+    // an object starting exactly at the span start never sees its start event:
+    // its stored checksum is the previous span's last dword (no object starts at
+    // a segment's offset 0)
+    if (kRec && u == 0 && Sr[0] == 0 && span != seg * d.spr)
+        stored = *reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(sg - 4);
 
     u32x4 buf[kStreamU];
 #pragma unroll
     for (int i = 0; i < kStreamU; i++)
-        buf[i] = load_step(uint64_t(i) < geo.sps ? uint64_t(i) : geo.sps - 1);
+        buf[i] = load_step(uint64_t(i) < sps ? uint64_t(i) : sps - 1);
 
-    for (uint64_t t0 = 0; t0 < geo.sps; t0 += kStreamU) {
+    for (uint64_t t0 = 0; t0 < sps; t0 += kStreamU) {
 #pragma unroll
         for (int ii = 0; ii < kStreamU; ii++) {
             const uint64_t t = t0 + ii;
-            if (t >= geo.sps)
+            if (t >= sps)
                 break;   // uniform
             u32x4 w = buf[ii];
             const uint64_t tn = t + kStreamU;
-            buf[ii] = load_step(tn < geo.sps ? tn : geo.sps - 1);
+            buf[ii] = load_step(tn < sps ? tn : sps - 1);
+            const uint32_t wr0 = w.x;   // dword 0 before the carry
             if (u == 0)
                 w.x ^= G;   // carry: the previous state injected into bytes 0..3
             const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
@@ -367,7 +553,7 @@ __global__ __launch_bounds__(kStreamWaves * kWaveSize, 1) void k_stream(StreamDe
                 }
                 int32_t nb = !Sd ? Sr[0] : (!Ed ? Er[0] : kBig);
                 int32_t P = grp_min(nb);
-                if (P == kBig && e0 + 64 < d.n && cnt == kStreamWin) {
+                if (P == kBig && e0 + 64 < e_hi && cnt == kStreamWin) {
                     // window used up (cnt is equal in the group then): next 64 entries
                     e0 += 64;
                     load_window();
@@ -431,14 +617,38 @@ __global__ __launch_bounds__(kStreamWaves * kWaveSize, 1) void k_stream(StreamDe
                                 d.xe_idx[span] = idx;
                                 xe_done = true;
                             } else {
-                                d.out[idx] = finalize ? ~raw : raw;
+                                const uint32_t res = finalize ? ~raw : raw;
+                                d.out[idx] = res;
+                                if (kRec && res != stored)   // src/ObjectManager.cc:659-663
+                                    atomicAdd(&d.vstat[seg].bad_objects, 1u);
                             }
                         }
                     }
-                    if (empty)   // Crc32C of no bytes: the initial state
+                    if (!kRec && empty)   // Crc32C of no bytes: the initial state
                         d.out[idx] = finalize ? 0u : 0xFFFFFFFFu;
-                    if (grp_or(isS ? 1u : 0u))   // re-base at the entry start, initial state injected
+                    if (grp_or(isS ? 1u : 0u)) {
+                        // re-base at the entry start, initial state injected
                         C = V ^ lds_u32(lds, kStrFfOff + 4 * d8);
+                        if (kRec) {
+                            // the object's stored checksum: the 4 bytes before S (step
+                            // positions p - 4 .. p - 1; below 0 they are the previous
+                            // step's bytes 124..127, held by lane 7)
+                            const int32_t q0 = int32_t(p) - 4;
+                            const int32_t d0 = q0 >> 2, d1 = (q0 + 3) >> 2;
+                            auto own = [&](int32_t dd) -> uint32_t {   // this lane's dword dd >> 3
+                                const int32_t j = dd >> 3;
+                                return j < 0 ? prev3 : (j == 0 ? wr0 : (j == 1 ? ws[1] : (j == 2 ? ws[2] : ws[3])));
+                            };
+                            const uint32_t gbase = uint32_t(lane) & ~7u;
+                            const uint32_t v0 = uint32_t(__builtin_amdgcn_ds_bpermute(
+                                int((gbase + (uint32_t(d0) & 7)) * 4), int(own(d0))));
+                            const uint32_t v1 = uint32_t(__builtin_amdgcn_ds_bpermute(
+                                int((gbase + (uint32_t(d1) & 7)) * 4), int(own(d1))));
+                            const uint32_t hdr = __builtin_amdgcn_alignbyte(v1, v0, uint32_t(q0) & 3);
+                            if (isS)
+                                stored = hdr;
+                        }
+                    }
                     Sd = Sd || isS;
                     Ed = Ed || isE;
                     if (Ed) {   // next slot
@@ -457,6 +667,7 @@ __global__ __launch_bounds__(kStreamWaves * kWaveSize, 1) void k_stream(StreamDe
                 }
             }
             G = grp_xor(F) ^ C;
+            prev3 = ws[3];
         }
     }
     // span end: the state (of an entry still open, or of the whole span) and the
@@ -472,30 +683,64 @@ __global__ __launch_bounds__(kStreamWaves * kWaveSize, 1) void k_stream(StreamDe
 
 // Entries that began in an earlier span: the state at their start span's end,
 // carried through the spans they cover, then the partial value of the span
-// where they end.
+// where they end.  Records mode: spans of the object's segment, and the
+// stored checksum compared (its header was in an earlier span).
+template <bool kRec>
 __global__ __launch_bounds__(256) void k_stream_fix(StreamDesc d)
 {
     const uint64_t g = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (g >= d.nspan || *d.bad_seq == d.seq)
         return;
-    const StreamGeo geo = stream_geo(d);
-    if (g * geo.sps >= geo.ns)
-        return;
-    const uint32_t i = d.xe_idx[g];
-    if (i == kNoIdx)
-        return;
-    uint64_t S, E;
-    stream_range(d, i, S, E);
-    const uint64_t sg = geo.A0 + g * geo.L;
-    // the span holding S: its group re-based there (an entry starting exactly at
-    // a span start had its initial state injected by that span's group)
-    const uint64_t h = (S - geo.A0) / geo.L;
-    uint32_t st = d.span_t[h];
-    if (h + 1 < g) {
-        const uint32_t cL = xpow8_any(geo.L);
-        for (uint64_t m = h + 1; m < g; m++)
-            st = mulmod_dev(st, cL) ^ d.span_t[m];
+    uint64_t S, E, sg, L, h, kg;
+    const uint32_t* span_t = d.span_t;
+    uint32_t i;
+    uint64_t seg = 0;
+    if (kRec) {
+        seg = g / d.spr;
+        if (seg >= d.nseg)
+            return;
+        const SegInfo gi = seg_info(d, seg);
+        if (!gi.ok)
+            return;
+        i = d.xe_idx[g];
+        if (i == kNoIdx)
+            return;
+        rec_range(d.rec[i], S, E);   // relative to the segment
+        L = gi.L;
+        kg = g - seg * d.spr;
+        sg = kg * L;
+        h = S / L;
+        span_t += seg * d.spr;
+    } else {
+        const StreamGeo geo = stream_geo(d);
+        if (g * geo.sps >= geo.ns)
+            return;
+        i = d.xe_idx[g];
+        if (i == kNoIdx)
+            return;
+        stream_range(d, i, S, E);
+        // the span holding S: its group re-based there (an entry starting exactly
+        // at a span start had its initial state injected by that span's group)
+        L = geo.L;
+        kg = g;
+        sg = geo.A0 + g * L;
+        h = (S - geo.A0) / L;
+    }
+    uint32_t st = span_t[h];
+    if (h + 1 < kg) {
+        const uint32_t cL = xpow8_any(L);
+        for (uint64_t m = h + 1; m < kg; m++)
+            st = mulmod_dev(st, cL) ^ span_t[m];
     }
     const uint32_t raw = mulmod_dev(st, xpow8_any(E - sg)) ^ d.xe_val[g];
-    d.out[i] = (d.flags & RAMCRC_FINALIZE) ? ~raw : raw;
+    const uint32_t res = (d.flags & RAMCRC_FINALIZE) ? ~raw : raw;
+    d.out[i] = res;
+    if (kRec) {
+        const uint64_t a = reinterpret_cast<uint64_t>(d.base) + seg * d.stride + S - 4;
+        const gu8* q = reinterpret_cast<const gu8*>(a);
+        const uint32_t stored = uint32_t(q[0]) | (uint32_t(q[1]) << 8) | (uint32_t(q[2]) << 16) |
+                                (uint32_t(q[3]) << 24);
+        if (res != stored)
+            atomicAdd(&d.vstat[seg].bad_objects, 1u);
+    }
 }

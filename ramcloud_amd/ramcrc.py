@@ -82,6 +82,7 @@ def lib():
         "ramcrc_stream_host": (i32, [vp, vp, u64, u64, vp, u32, i32, i32]),
         "ramcrc_segment_walk_device": (i32, [vp, vp, u64, u32, u64, vp, vp, vp, u64, vp, vp]),
         "ramcrc_verify_objects_device": (i32, [vp, vp, u64, vp, u64, vp, vp, vp, vp]),
+        "ramcrc_verify_objects_ordered_device": (i32, [vp, vp, u64, u64, vp, u64, vp, vp, vp, vp]),
         "ramcrc_segments_certify_device": (i32, [vp, vp, u64, u32, u64, vp, vp, vp, vp]),
         "ramcrc_segment_fill_objects": (i32, [vp, u32, u32, u64, _c.POINTER(u32), vp]),
         "ramcrc_assemble_objects_device": (i32, [vp, vp, vp, vp, vp, u64, vp]),
@@ -360,8 +361,17 @@ class Context:
         _check(rc, "ramcrc_segments_certify_device")
         return certs
 
-    def verify_objects(self, data, seg_stride, entries, n_entries, obj_crc, status, stream=None):
-        """Object::computeChecksum + comparison for every object record of a walk."""
+    def verify_objects(self, data, seg_stride, entries, n_entries, obj_crc, status, stream=None,
+                       nseg=None):
+        """Object::computeChecksum + comparison for every object record of a walk.
+        nseg given: the ordered pass over each segment
+        (ramcrc_verify_objects_ordered_device); else object by object."""
+        if nseg is not None:
+            rc = lib().ramcrc_verify_objects_ordered_device(
+                self._h, _ptr(data), seg_stride, int(nseg), _ptr(entries), entries.shape[0],
+                _ptr(n_entries), _ptr(obj_crc), _ptr(status), _stream(stream))
+            _check(rc, "ramcrc_verify_objects_ordered_device")
+            return status
         rc = lib().ramcrc_verify_objects_device(self._h, _ptr(data), seg_stride, _ptr(entries),
                                                 entries.shape[0], _ptr(n_entries), _ptr(obj_crc),
                                                 _ptr(status), _stream(stream))
