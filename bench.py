@@ -726,6 +726,8 @@ def run_replay(args, ranks):
     ctx = ramcrc.Context(ranks.local)
     if args.serial_walk:
         ctx.set_serial_walk(True)
+    if args.walk_part_shift:
+        ctx.set_walk_part_shift(args.walk_part_shift)
     seg = args.seg_mib * MiB
     nseg = args.replay_nseg
     d = torch.empty(nseg * seg, dtype=torch.uint8, device="cuda")
@@ -777,7 +779,10 @@ def run_replay(args, ranks):
                                f"{args.value_len} B-value objects",
                    "pipeline": (f"walk on {args.walk_cus} CUs beside the scan of the previous batch"
                                 if args.walk_cus else "none"),
-                   "walk": "serial (one wave per segment)" if args.serial_walk else "parallel (64 KiB parts)",
+                   "walk": ("serial (one wave per segment)" if args.serial_walk else
+                            f"parallel ({1 << (args.walk_part_shift - 10)} KiB parts, forced)"
+                            if args.walk_part_shift else
+                            "parallel (part size from the entry density, k_walk_probe)"),
                    "objects": int(counts.sum()), "object_bytes_checksummed": obj_bytes},
         "roofline": {"bound": "hbm", "kernel": "k_entries (object verify)",
                      "achieved": round(achieved, 1) if achieved else None,
@@ -920,9 +925,11 @@ def parse_args(argv=None):
     ap.add_argument("--seg-kib", type=int, default=0, help="--host-dry-run: segment KiB")
     ap.add_argument("--value-len", type=int, default=1024,
                     help="config 4 / replay: object value bytes (RecoverSegmentBenchmark default)")
+    ap.add_argument("--walk-part-shift", type=int, default=0,
+                    help="replay: force log2 of the parallel walk's part bytes (0: chosen per batch)")
     ap.add_argument("--entries", type=int, default=1_000_000)
     ap.add_argument("--path", default="entries", choices=["entries", "batch"])
-    ap.add_argument("--order", default="log", choices=["log", "any"],
+    ap.add_argument("--order", default="any", choices=["log", "any"],
                     help="entries config: log = RAMCRC_ORDERED stream pass (the entries are "
                          "packed in log order); any = the binned path for arbitrary tables")
     ap.add_argument("--entry-size", type=int, default=0, help="fixed entry length (default: Zipf mix)")

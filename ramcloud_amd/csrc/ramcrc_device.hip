@@ -3221,7 +3221,8 @@ struct PWalk {
     uint32_t* fallback;   // per segment: nonzero = walked by k_seg_walk
     uint64_t* seg_base;   // per segment: first record slot (B)
     uint2* recs;          // per part: kPartRec records of A's walk {offset, length << 8 | header}
-    uint32_t pshift;      // log2 part bytes of this launch
+    uint32_t pshift;      // log2 part bytes of this launch (from *geo when geo is set)
+    const uint32_t* geo;  // the part shift k_walk_probe chose for this batch
     // A's records past the first kPartRec of a part: blocks of kPartRec from a
     // pool (one atomic per block), up to kMaxBlocks per part
     uint2* pool;
@@ -3275,6 +3276,72 @@ __device__ __forceinline__ uint32_t walk_limit(const PWalk& w, uint64_t seg)
     return len < w.capacity ? len : w.capacity;
 }
 
+// The part geometry of this batch: every walk kernel takes it from the word
+// k_walk_probe wrote (the host sizes its grids and scratch for the smallest
+// part the probe may choose).
+__device__ __forceinline__ PWalk walk_geo(PWalk w)
+{
+    if (w.geo) {
+        w.pshift = *w.geo;
+        w.nparts = uint32_t((uint64_t(w.capacity) + (1ull << w.pshift) - 1) >> w.pshift);
+    }
+    return w;
+}
+
+// Part size per batch from the entry density.  A part should hold about 64
+// entries: much fewer and the sync search (which stages the first 7 KiB of
+// a part and chases 6 hops) mostly finds no header or chases far through
+// global memory, and k_walk_fix re-walks the part; much more and the one-lane
+// part walks get long (profiles/r04/parts: 8 KiB values 1.90 TB/s with 64 KiB
+// parts, 3.85 with 512 KiB; 64 B values 1.25 with 64 KiB, 0.78 with 128 KiB).
+// One wave: lane l walks the first kProbeHops entries of one of up to 64
+// segments spread over the batch; the mean entry size m gives the shift
+// round(log2(64 m)) within [kPartShift, kPartShiftMax].  A forced shift
+// (RAMCRC_OPT_WALK_PART_SHIFT) is written as is.
+constexpr uint32_t kPartShiftMax = 20;
+constexpr int kProbeHops = 8;
+
+__global__ __launch_bounds__(kWaveSize) void k_walk_probe(PWalk w, uint32_t forced, uint32_t* geo)
+{
+    const int lane = threadIdx.x;
+    const uint64_t ns = w.nseg < uint64_t(kWaveSize) ? w.nseg : uint64_t(kWaveSize);
+    uint64_t dist = 0, hops = 0;
+    if (!forced && uint64_t(lane) < ns) {
+        const uint64_t seg = uint64_t(lane) * w.nseg / ns;
+        const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
+        const uint32_t limit = walk_limit(w, seg);
+        uint32_t pos = 0;
+        for (int hh = 0; hh < kProbeHops && pos < limit; hh++) {
+            const uint64_t q = seg_peek(sb, pos, w.capacity);
+            const Hop h = hop_of(q, pos);
+            if (!plausible(q, h, w.capacity) || h.next > limit)
+                break;
+            dist += h.next - pos;
+            hops++;
+            pos = uint32_t(h.next);
+        }
+    }
+#pragma unroll
+    for (int o = 1; o < kWaveSize; o <<= 1) {
+        dist += __shfl_xor(dist, o, kWaveSize);
+        hops += __shfl_xor(hops, o, kWaveSize);
+    }
+    if (lane == 0) {
+        uint32_t shift = kPartShift;
+        if (forced) {
+            shift = forced;
+        } else if (hops) {
+            const uint64_t t = 64 * (dist / hops);   // bytes of 64 entries
+            uint32_t l = 63 - uint32_t(__builtin_clzll(t | 1));   // floor(log2 t)
+            // round to nearest in log scale: up when t >= 2^l * sqrt(2)
+            if (t * t >= (1ull << (2 * l)) * 2)
+                l++;
+            shift = l < kPartShift ? kPartShift : (l > kPartShiftMax ? kPartShiftMax : l);
+        }
+        *geo = shift;
+    }
+}
+
 // A0: one wave per part k >= 1.  The part's first kSyncWin bytes are staged
 // in LDS, so most candidate hops (the true chain's included, for entries of
 // a few KiB) read LDS instead of waiting on global memory.
@@ -3325,8 +3392,9 @@ __device__ __forceinline__ SyncPart sync_part(const PWalk& w, uint64_t i)
 #define RAMCRC_SYNC_EARLY 1   // stop at the end of the first round holding a survivor
 #endif
 
-__global__ __launch_bounds__(kSyncWaves * kWaveSize) void k_walk_sync(PWalk w)
+__global__ __launch_bounds__(kSyncWaves * kWaveSize) void k_walk_sync(PWalk w0)
 {
+    const PWalk w = walk_geo(w0);
     __shared__ __attribute__((aligned(16))) uint8_t wins[kSyncWaves][kSyncStage];
     __shared__ uint16_t lists[kSyncWaves][kSyncRound];   // a round's first-hop survivors
     constexpr uint32_t kSU = kSyncStage / 1024;
@@ -3646,8 +3714,9 @@ __device__ __forceinline__ void walk_tab_fill(uint32_t* tab)
 // 16 MiB or more, is marked kPartSpill and walked again by C; its first
 // kPartRec records still go to the scratch (B meets a misguessed chain within
 // its first few entries), unless an entry's length does not fit a record.
-__global__ __launch_bounds__(256) void k_walk_parts(PWalk w)
+__global__ __launch_bounds__(256) void k_walk_parts(PWalk w0)
 {
+    const PWalk w = walk_geo(w0);
     __shared__ uint32_t tab[4 * 256];
     __shared__ uint2 lrec[256][kPartRec];
     walk_tab_fill(tab);
@@ -3752,8 +3821,9 @@ __device__ unsigned long long g_fixdbg[8];
 // after it.  The accepted parts' metadata CRCs fold into the segment's with
 // one GF(2) multiply per part, then the status is written and the records
 // are allocated (one atomic per segment).
-__global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
+__global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w0)
 {
+    const PWalk w = walk_geo(w0);
     __shared__ uint32_t tab[4 * 256];
     __shared__ __attribute__((aligned(16))) uint8_t win[kFixWin];
     walk_tab_fill(tab);
@@ -4249,8 +4319,9 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_fix(PWalk w)
 // instruction.  Entries walked by k_walk_fix before it met the guessed chain
 // are walked once more here; parts walked again in full, or with more
 // records than the scratch holds, are walked again here in full.
-__global__ __launch_bounds__(256) void k_walk_emit(PWalk w)
+__global__ __launch_bounds__(256) void k_walk_emit(PWalk w0)
 {
+    const PWalk w = walk_geo(w0);
     __shared__ uint32_t tab[4 * 256];
     walk_tab_fill(tab);
     const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -4289,8 +4360,9 @@ __global__ __launch_bounds__(256) void k_walk_emit(PWalk w)
 // each level's loads for all of them together.
 static_assert(kPartRec == kWaveSize, "k_walk_copy: one lane per record of a block");
 constexpr int kCopyU = 4;
-__global__ __launch_bounds__(256) void k_walk_copy(PWalk w)
+__global__ __launch_bounds__(256) void k_walk_copy(PWalk w0)
 {
+    const PWalk w = walk_geo(w0);
     const uint64_t nfirst = w.nseg * w.nparts;
     const uint64_t used = *w.pool_used;
     const uint64_t nblk = nfirst + (used < w.pool_cap ? used : w.pool_cap);
@@ -5140,9 +5212,9 @@ int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_s
         // parallel walk: sync search, part walks, per-segment fix-up, record
         // emission; the serial walker then takes only the segments the fix-up
         // handed back (uint32_t wraps, exhausted re-walk budget)
-        // part size (RAMCRC_OPT_WALK_PART_SHIFT): smaller parts do not pay on
-        // dense segments -- A and C then read a cache line per entry header
-        // and are bound by those fetches, not by their chains
+        // part size: chosen per batch on the device by k_walk_probe from the
+        // entry density (or forced, RAMCRC_OPT_WALK_PART_SHIFT); grids and
+        // scratch are sized for the smallest part it may choose
         const uint32_t pshift = c->walk_pshift ? c->walk_pshift : kPartShift;
         const uint32_t nparts = uint32_t((uint64_t(seg_capacity) + (1ull << pshift) - 1) >> pshift);
         const uint64_t total = n_seg * uint64_t(nparts);
@@ -5167,8 +5239,8 @@ int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_s
             rc = grow_device(reinterpret_cast<void**>(&c->walk_blocks), &c->walk_blocks_cap,
                              total * kMaxBlocks, sizeof(uint32_t));
         if (!rc)
-            rc = grow_device(reinterpret_cast<void**>(&c->walk_pool_used), &c->walk_pool_used_cap, 1,
-                             sizeof(unsigned long long));
+            rc = grow_device(reinterpret_cast<void**>(&c->walk_pool_used), &c->walk_pool_used_cap, 2,
+                             sizeof(unsigned long long));   // [1]: the part shift word
         if (rc)
             return rc;
         PWalk pw{};
@@ -5187,12 +5259,16 @@ int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_s
         pw.seg_base = c->walk_base;
         pw.recs = static_cast<uint2*>(c->walk_recs);
         pw.pshift = pshift;
+        uint32_t* geo = reinterpret_cast<uint32_t*>(c->walk_pool_used + 1);
+        pw.geo = geo;
         pw.pool = static_cast<uint2*>(c->walk_pool);
         pw.pool_owner = c->walk_pool_owner;
         pw.blocks = c->walk_blocks;
         pw.pool_used = c->walk_pool_used;
         pw.pool_cap = pool_blocks;
         HIPCHK(hipMemsetAsync(c->walk_pool_used, 0, sizeof(unsigned long long), s));
+        hipLaunchKernelGGL(k_walk_probe, dim3(1), dim3(kWaveSize), 0, s, pw, c->walk_pshift, geo);
+        HIPCHK(hipGetLastError());
         if (nparts > 1) {
             uint64_t g0 = (total + kSyncWaves - 1) / kSyncWaves;
             if (g0 > uint64_t(8) * c->ncu)

@@ -102,7 +102,7 @@ class RecoveryVerify:
     kernels ran on the current stream."""
 
     def __init__(self, ctx, nseg, capacity, stride=None, entries_cap=None, min_entry=None,
-                 ordered=True):
+                 ordered=False):
         self.ctx = ctx
         # ordered: objects checked in one pass over each segment
         # (ramcrc_verify_objects_ordered_device); False: object by object
