@@ -23,7 +23,7 @@ def main(db, pats):
         print(f"{n[:60]:60s} calls={len(v):4d} avg_us={sum(v) / len(v) / 1e3:10.2f} "
               f"pct={100 * sum(v) / tot:5.1f}")
     ccols = [r[1] for r in c.execute("pragma table_info(counters_collection)")]
-    if not ccols:
+    if not ccols or "counter_value" not in ccols:
         return
     cname = "kernel_name" if "kernel_name" in ccols else "name"
     vals = defaultdict(lambda: defaultdict(list))
