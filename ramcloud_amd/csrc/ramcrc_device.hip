@@ -826,14 +826,18 @@ __global__ __launch_bounds__(256) void k_combine(BatchDesc d, Plan pl, uint64_t 
     }
     if (pl.group_pref[pl.ngroups] == 0)
         return;   // no large buffer in this launch
-    const uint64_t i = wave * kWaveSize + lane;
-    uint64_t S = 0, E = 0;
-    const bool big = i < n && buffer_range<kMode>(d, i, S, E) && is_large(E - S);
-    uint64_t todo = __ballot(big);
-    while (todo) {
-        const int j = __builtin_ctzll(todo);
-        todo &= todo - 1;
-        combine_one<kMode>(d, pl, per_seg, wave * kWaveSize + j, shfl64(S, j), shfl64(E, j), lane);
+    // waves of 64 entries, grid-stride (capped grid, as k_plan_count)
+    const uint64_t nwave = uint64_t(gridDim.x) * (256 / kWaveSize);
+    for (uint64_t wv = wave; wv * kWaveSize < n; wv += nwave) {
+        const uint64_t i = wv * kWaveSize + lane;
+        uint64_t S = 0, E = 0;
+        const bool big = i < n && buffer_range<kMode>(d, i, S, E) && is_large(E - S);
+        uint64_t todo = __ballot(big);
+        while (todo) {
+            const int j = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            combine_one<kMode>(d, pl, per_seg, wv * kWaveSize + j, shfl64(S, j), shfl64(E, j), lane);
+        }
     }
 }
 
@@ -861,6 +865,13 @@ constexpr int kNB = 161;                   // step-count bins
 #endif
 constexpr int kEntWaves = RAMCRC_ENT_WAVES;   // k_entries: waves per workgroup (1 per CU)
 constexpr int kSmallK = RAMCRC_SMALLK;     // bins 2..kSmallK: octets loaded one ahead
+#ifndef RAMCRC_TINY_K
+#define RAMCRC_TINY_K 4
+#endif
+// bins 2 .. kTinyK (entries of 2 .. kTinyK windows, e.g. objects of 129 ..
+// ~500 B): the multi-window tiny phase (tiny_run_cf<true>); 1 = off (the short bins)
+constexpr int kTinyK = RAMCRC_TINY_K;
+static_assert(kTinyK >= 1 && kTinyK <= 4, "tiny windows: e_tot fits 10 bits");
 #ifndef RAMCRC_ENT_NT
 #define RAMCRC_ENT_NT 1
 #endif
@@ -964,7 +975,7 @@ struct BinCounters {
     uint64_t cursor[kNB];     // scatter cursors, relative to start
     uint32_t hist[kNB];       // entry counts
     uint32_t nlarge;          // large buffers the count pass left to k_chunks (skip_large)
-    uint32_t pad_;
+    uint32_t ninact;          // inactive records (records mode: not checked here)
 };
 
 struct BinTable {
@@ -1068,7 +1079,7 @@ template <int kMode>
 __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, int skip_large)
 {
     __shared__ uint32_t h[kNB];
-    __shared__ uint32_t nlarge;
+    __shared__ uint32_t nlarge, ninact;
     BinCounters& ctr = so.bt->ctr[so.par];
     if (blockIdx.x == 0) {
         // the next sequence's counters (see BinCounters)
@@ -1077,13 +1088,17 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
             nx.cursor[t] = 0;
             nx.hist[t] = 0;
         }
-        if (threadIdx.x == 0)
+        if (threadIdx.x == 0) {
             nx.nlarge = 0;
+            nx.ninact = 0;
+        }
     }
     for (int t = threadIdx.x; t < kNB; t += blockDim.x)
         h[t] = 0;
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0) {
         nlarge = 0;
+        ninact = 0;
+    }
     __syncthreads();
     const uint64_t tile = uint64_t(blockDim.x) * kBinPer;
     const uint64_t n = entry_count<kMode>(d);
@@ -1096,11 +1111,12 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
             S[q] = E[q] = 0;
             act[q] = i < n && buffer_range<kMode>(d, i, S[q], E[q]);
         }
-        uint32_t big = 0;
+        uint32_t big = 0, inact = 0;
 #pragma unroll
         for (int q = 0; q < kBinPer; q++) {
             const bool large = skip_large && is_large(E[q] - S[q]);
             big += act[q] && large;
+            inact += !act[q] && base + uint64_t(q) * blockDim.x + threadIdx.x < n;
             const bool active = act[q] && !large;
             const int b = active ? bin_of(S[q], E[q]) : 0;
             uint32_t unused;
@@ -1110,6 +1126,10 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
             if (big)
                 atomicAdd(&nlarge, big);
         }
+        if (kMode == kRecords && __ballot(inact != 0)) {
+            if (inact)
+                atomicAdd(&ninact, inact);
+        }
     }
     __syncthreads();
     for (int t = threadIdx.x; t < kNB; t += blockDim.x)
@@ -1117,6 +1137,8 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
             atomicAdd(&ctr.hist[t], h[t]);
     if (threadIdx.x == 0 && nlarge)
         atomicAdd(&ctr.nlarge, nlarge);
+    if (threadIdx.x == 0 && ninact)
+        atomicAdd(&ctr.ninact, ninact);
 }
 
 // Bin layout from the histogram, computed by every k_bin_scatter workgroup
@@ -1146,7 +1168,7 @@ __device__ __forceinline__ bool bin_layout(const Sorted& so, BinScratch& sc, boo
     const BinCounters& ctr = bt->ctr[so.par];
     const int b = threadIdx.x, lane = b & 63, w = b >> 6;
     if (threadIdx.x == 0)
-        sc.direct = direct_n && uint64_t(ctr.hist[0]) + ctr.hist[1] == direct_n;
+        sc.direct = direct_n && uint64_t(ctr.hist[0]) + ctr.hist[1] + ctr.ninact == direct_n;
     __syncthreads();
     const bool direct = sc.direct;
     if (publish && threadIdx.x == 0)
@@ -1159,7 +1181,7 @@ __device__ __forceinline__ bool bin_layout(const Sorted& so, BinScratch& sc, boo
         }
         const uint64_t oct = (cnt + kG - 1) / kG;
         pos_c = oct * kG;
-        item_c = b >= 2 ? oct * (kc + kOctetCost) : 0;   // bins 0-1: the tiny phase
+        item_c = b > kTinyK && b >= 2 ? oct * (kc + kOctetCost) : 0;   // bins 0..kTinyK: tiny phases
         ps = pos_c;
         is = item_c;
 #pragma unroll
@@ -1224,7 +1246,8 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter(BatchDesc d, Sorted so
     __shared__ BinScratch sc;
     for (int t = threadIdx.x; t < kNB; t += blockDim.x)
         cnt[t] = 0;
-    if (!bin_layout(so, sc, blockIdx.x == 0, (kMode == kTable && RAMCRC_TINY_CF) ? d.n : 0))
+    if (!bin_layout(so, sc, blockIdx.x == 0,
+                    (kMode == kTable || kMode == kRecords) && RAMCRC_TINY_CF ? entry_count<kMode>(d) : 0))
         return;   // corrupted histogram: nothing is scattered, k_entries refuses
     if (sc.direct)
         return;   // all tiny: k_entries reads the table in place
@@ -1605,7 +1628,7 @@ __device__ unsigned long long g_stamps[kStampWaves * kStampSlots];
     } while (0)
 #endif
 
-// The tiny phase with conflict-free table lookups (RAMCRC_TINY_CF).  The
+// The tiny phases with conflict-free table lookups (RAMCRC_TINY_CF).  The
 // position table is laid out column-major, byte address 512 (255 - b) +
 // 4 (128 - m) for X^m(b) (g_tab.post), so a lookup's LDS bank is (128 - m)
 // mod 32 whatever the data byte.  Lane u of a group holds the window dwords
@@ -1617,14 +1640,111 @@ __device__ unsigned long long g_stamps[kStampWaves * kStampSlots];
 // 4 residue classes: the 32 lanes of a ds_read_b32 group hit 32 banks.  Bytes
 // outside the entry are masked to 0 and complemented to column 255, whose
 // rows, and the 128 words after the table, are zero; so no zero rows and
-// no clamps are needed.  Round structure, descriptor ownership and the init
-// fold are those of tiny_run, and so is the return value.
+// no clamps are needed.
+//
+// tiny_run_cf: bins 0-1, entries of one 128-byte window (all 100-byte log
+// entries).  tiny_multi: bins 2 .. kTinyK, entries of 2 .. kTinyK windows
+// (objects of about 129 .. 500 B): window by window with Horner between them,
+//   acc = X^e_w(acc) ^ R_w,
+// R_w the group's sum over window w's bytes at their distance from the
+// window's end e_w (128 for all but the last), X^e (e >= 4) four lookups in the
+// same table by lanes gl & 3 and two quad swaps; an entry whose last window
+// would hold only 1 .. 3 bytes stops a window early and its owner takes those
+// bytes bytewise.  (The short-bin loop of entries_run spends an octet's head
+// masks, fold and unpad multiply -- about 600 VALU per octet of 2-step entries
+// -- where this spends the windows.)
+//
+// Round r of a wave covers 64 sorted slots; lane L owns slot 64 r + L: it loads
+// that slot's descriptor two rounds ahead (one coalesced load per round instead
+// of eight group-redundant ones; tiny_multi derives the entry geometry from it
+// one round later), and at the end folds in the slot's initial state and
+// stores the result.  Group g hashes the entries
+// of lanes 8 g .. 8 g + 7 in turn, reading each owner's window (base, offset,
+// length) by swizzle within the group; tiny_run_cf loads a round's windows one
+// round ahead, tiny_multi an entry's windows one entry ahead.
+struct TinyRaw {
+    u32x4 dd;            // sorted descriptor {S, E}, or {off, len} on the direct path
+    uint32_t ix, init;
+};
+
+struct TinyCf {
+    uint64_t S;
+    // E - A (bits 0-9; 0: nothing to hash, or bytewise), S - A (10-13), window
+    // page-safe (14), E - S (16-25); A = S rounded down to 16
+    uint32_t geo;
+    uint32_t ix, init;
+};
+
+// windows hashed for an entry of geometry geo (tiny_multi: the last 1 .. 3
+// bytes past a window go bytewise, as X^e needs e >= 4)
+__device__ __forceinline__ uint32_t tk_tail(uint32_t geo)
+{
+    const uint32_t t = geo & 127u;
+    return geo > 128 && t != 0 && t < 4 ? t : 0u;
+}
+
+__device__ __forceinline__ uint32_t tk_windows(uint32_t geo)
+{
+    return ((geo & 0x3FFu) - tk_tail(geo) + 127u) >> 7;
+}
+
+// The group's sum over one window's bytes in [sa, e), each byte b at window
+// offset o as X^(e - o)(b) (all 8 lanes of the group get it).
+__device__ __forceinline__ uint32_t tiny_win_hash(const uint8_t* lds, const u32x4& wv, uint32_t sa,
+                                                  uint32_t e, uint32_t gl, uint32_t g4)
+{
+    const uint32_t c = (e + g4) & 3;                  // byte rotation of this group
+    const uint32_t bb = 512 - 4 * e + 16 * gl;        // 4 (128 - e + 4 u): row of offset 4 u
+    const uint32_t rot = __builtin_amdgcn_alignbyte(0x0C080400u, 0x0C080400u, c);
+    // byte k of the rotated dword sits at window offset 4 u + ((k + c) & 3)
+    // (row bits below 512 for every byte of the entry; a masked byte's
+    // column 255 is zero at every row, so OR-ing its larger row is safe)
+    uint32_t pk[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        pk[k] = bb + ((rot >> (8 * k)) & 0xFF);
+    // tail: dword j keeps its bytes before E, clamp(e - 32 j - 4 u, 0, 4)
+    const int z = 32 - 8 * int(e) + 32 * int(gl);   // bits to drop from dword 0's top
+    // head: window bytes before S lie in dword 0 of lanes 0-3
+    const uint32_t hd = uint32_t(min(max(8 * (int(sa) - 4 * int(gl)), 0), 32));
+    const uint32_t ws[4] = {wv.x, wv.y, wv.z, wv.w};
+    uint32_t v[16];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t sh = uint32_t(min(max(z + 256 * j, 0), 32));
+        uint32_t keep = uint32_t(uint64_t(0xFFFFFFFFu) >> sh);
+        if (j == 0)
+            keep &= uint32_t(~uint64_t(0) << hd);
+        const uint32_t xb = ~(ws[j] & keep);          // masked bytes -> column 255
+        const uint32_t xr = __builtin_amdgcn_alignbyte(xb, xb, c);
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            v[4 * j + k] = *reinterpret_cast<const uint32_t*>(
+                lds + ((((xr >> (8 * k)) & 0xFF) << 9) | pk[k]) + 128 * j);
+    }
+    const uint32_t t0 = xor3(v[0], v[1], v[2]), t1 = xor3(v[3], v[4], v[5]);
+    const uint32_t t2 = xor3(v[6], v[7], v[8]), t3 = xor3(v[9], v[10], v[11]);
+    const uint32_t t4 = xor3(v[12], v[13], v[14]);
+    uint32_t R = xor3(xor3(t0, t1, t2), xor3(t3, t4, v[15]), 0u);
+    R ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(R), 0xB1, 0xF, 0xF, false));   // lane ^ 1
+    R ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(R), 0x4E, 0xF, 0xF, false));   // lane ^ 2
+    R ^= uint32_t(__builtin_amdgcn_ds_swizzle(int(R), 0x1F | (4 << 10)));           // lane ^ 4
+    return R;
+}
+
 __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so, uint8_t* lds,
-                                            bool bad, uint32_t blk, uint32_t nblk)
+                                            bool bad, uint32_t blk, uint32_t nblk, bool need_table)
 {
     const uint64_t direct_n = so.bt->direct_n;   // all tiny: the caller's table, in place
-    if (!direct_n && so.bt->start[2] == so.bt->start[0])
-        return true;   // no entry of at most one window (uniform: every wave exits)
+    if (!direct_n && so.bt->start[2] == so.bt->start[0]) {
+        // no entry of at most one window (uniform: every wave exits); the
+        // multi-window phase still needs the table
+        if (need_table) {
+            fill_plain(lds, 0, g_tab.post, 256 * 128 + 128);
+            return !__syncthreads_or(bad);
+        }
+        return true;
+    }
     const int lane = threadIdx.x & (kWaveSize - 1);
     const uint32_t gl = uint32_t(lane) & 7;
     const uint32_t g4 = (uint32_t(lane) >> 3) & 3;
@@ -1644,14 +1764,21 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
         o.ix = kNoIdx;
         o.init = 0xFFFFFFFFu;
         if (r < rounds && sl < s1) {
-            if (direct_n) {   // kTable: buffer sl = base + off[sl], len[sl]
-                const uint64_t S = reinterpret_cast<uint64_t>(d.base) + d.off[sl];
-                const uint64_t E = S + d.len[sl];
-                dd = u32x4{uint32_t(S), uint32_t(S >> 32), uint32_t(E), uint32_t(E >> 32)};
-                o.ix = uint32_t(sl);
+            if (direct_n) {   // kTable: buffer sl = base + off[sl], len[sl]; records: record sl
+                uint64_t S, E;
+                bool act = true;
+                if (d.rec) {
+                    act = buffer_range<kRecords>(d, sl, S, E);
+                } else {
+                    S = reinterpret_cast<uint64_t>(d.base) + d.off[sl];
+                    E = S + d.len[sl];
+                }
+                if (act)
+                    dd = u32x4{uint32_t(S), uint32_t(S >> 32), uint32_t(E), uint32_t(E >> 32)};
+                o.ix = act ? uint32_t(sl) : kNoIdx;
                 if (d.init)
                     o.init = d.init[sl];
-                if (E - S >= 4 && E - (S & ~uint64_t(15)) > kStep) {
+                if (act && E - S >= 4 && E - (S & ~uint64_t(15)) > kStep) {
                     // not tiny after all: the histogram lied; refuse, write nothing
                     atomicOr(so.status, kStatusSticky | kStatusBins);
                     o.ix = kNoIdx;
@@ -1805,6 +1932,165 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
     return true;
 }
 
+// bins 2 .. kTinyK (see above): one entry per q as in tiny_run_cf, all K
+// windows of the group's next entry loaded while the current one is hashed
+// (two buffers of kTinyK windows instead of a round of first windows).
+__device__ __forceinline__ void tiny_multi(const BatchDesc& d, const Sorted& so, const uint8_t* lds,
+                                           uint32_t blk, uint32_t nblk)
+{
+    const uint64_t s0 = so.bt->start[2], s1 = so.bt->start[kTinyK + 1];
+    if (kTinyK < 2 || s0 == s1)
+        return;   // uniform
+    const int lane = threadIdx.x & (kWaveSize - 1);
+    const uint32_t gl = uint32_t(lane) & 7;
+    const uint32_t g4 = (uint32_t(lane) >> 3) & 3;
+    const uint64_t wave = uint64_t(blk) * kEntWaves +
+                          __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
+    const uint64_t nwaves = uint64_t(nblk) * kEntWaves;
+    const uint64_t rounds = (s1 - s0 + 63) / 64;
+    if (wave >= rounds)
+        return;   // uniform
+    const bool finalize = d.flags & RAMCRC_FINALIZE;
+    const uint64_t dummy = reinterpret_cast<uint64_t>(so.bt);
+    typedef const __attribute__((address_space(1))) uint32_t g32;
+
+    auto load_raw = [&](uint64_t r) -> TinyRaw {
+        TinyRaw w;
+        const uint64_t sl = s0 + r * 64 + uint32_t(lane);
+        const bool in = r < rounds && sl < s1;
+        const uint64_t sc = in ? sl : s0;
+        w.dd = so.desc[sc];
+        const uint32_t ix = so.idx[sc];
+        w.ix = in ? ix : kNoIdx;
+        w.init = d.init ? so.init[sc] : 0xFFFFFFFFu;
+        return w;
+    };
+    auto own_of = [&](const TinyRaw& w) -> TinyCf {
+        TinyCf o;
+        o.ix = w.ix;
+        o.init = w.init;
+        uint64_t S = (uint64_t(w.dd.y) << 32) | w.dd.x, E = (uint64_t(w.dd.w) << 32) | w.dd.z;
+        if (o.ix == kNoIdx)
+            S = E = dummy;
+        o.S = S;
+        const uint32_t len = uint32_t(E - S);
+        const uint64_t A = S & ~uint64_t(15);
+        o.geo = (len >= 4 ? uint32_t(E - A) : 0u) | (uint32_t(S - A) << 10) | (len << 16);
+        return o;
+    };
+    // the owner's stored object checksum (records mode) and the word holding
+    // the entry's last three bytes (its bytewise tail), a round ahead
+    auto own_loads = [&](const TinyCf& o, uint32_t& st, uint32_t& tw) {
+        st = d.vstat && o.ix != kNoIdx ? load_u32_any(o.S - 4) : 0u;
+        const uint64_t E = o.S + ((o.geo >> 16) & 0x3FF);
+        const uint64_t a = o.ix != kNoIdx ? E - 3 : dummy;   // entries here hold >= 113 bytes
+        const uint64_t b = o.ix != kNoIdx ? E - 1 : dummy;
+        const uint32_t w0 = *reinterpret_cast<g32*>(a & ~uint64_t(3));
+        const uint32_t w1 = *reinterpret_cast<g32*>(b & ~uint64_t(3));
+        tw = __builtin_amdgcn_alignbyte(w1, w0, uint32_t(a) & 3);   // bytes E - 3, E - 2, E - 1
+    };
+    auto tabv = [&](uint32_t m, uint32_t b) -> uint32_t {
+        return *reinterpret_cast<const uint32_t*>(lds + 512 * (255 - b) + 4 * (128 - m));
+    };
+    auto xshift = [&](uint32_t v, uint32_t m) -> uint32_t {   // X^m(v), 4 <= m <= 128
+        return xor3(tabv(m, v & 0xFF), tabv(m - 1, (v >> 8) & 0xFF), tabv(m - 2, (v >> 16) & 0xFF)) ^
+               tabv(m - 3, v >> 24);
+    };
+    // the windows of the entry (geo, S) into w: window k is [A + 128 k, + 128);
+    // a dword at or past the window's last entry byte reads that byte's dword
+    auto load_entry = [&](uint32_t geo, uint64_t S, u32x4 (&w)[kTinyK]) {
+        const uint32_t K = tk_windows(geo);
+        const uint32_t el = (geo & 0x3FF) - tk_tail(geo) - 128 * (K - 1);   // last window's end
+        const uint64_t au = (S & ~uint64_t(15)) + 4 * gl;
+#pragma unroll
+        for (int k = 0; k < kTinyK; k++) {
+            if (uint32_t(k) < K) {
+                const uint32_t e = uint32_t(k) + 1 == K ? el : 128u;
+                const int lim = (max(int(e) - 1, 0) & ~3) - int(4 * gl);
+                const uint64_t aw = au + 128 * uint64_t(k);
+                w[k].x = *reinterpret_cast<g32*>(aw + min(0, lim));
+                w[k].y = *reinterpret_cast<g32*>(aw + min(32, lim));
+                w[k].z = *reinterpret_cast<g32*>(aw + min(64, lim));
+                w[k].w = *reinterpret_cast<g32*>(aw + min(96, lim));
+            }
+        }
+    };
+
+    uint64_t r = wave;
+    TinyRaw w1 = load_raw(r + nwaves);
+    TinyCf o0 = own_of(load_raw(r));
+    uint32_t sc, tc;
+    own_loads(o0, sc, tc);
+    u32x4 buf[2][kTinyK];
+    uint32_t gq[2];
+    gq[0] = swz_from<0>(o0.geo);
+    load_entry(gq[0], (uint64_t(swz_from<0>(uint32_t(o0.S >> 32))) << 32) | swz_from<0>(uint32_t(o0.S)),
+               buf[0]);
+    for (; r < rounds; r += nwaves) {
+        const TinyRaw w2 = load_raw(r + 2 * nwaves);
+        const TinyCf o1 = own_of(w1);   // loaded a round ago
+        const bool more = r + nwaves < rounds;
+        uint32_t sn = 0, tn = 0;
+        own_loads(o1, sn, tn);
+        uint32_t mine = 0;
+        static_for8([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            // the group's next entry: q + 1 of this round, or q 0 of the next
+            {
+                constexpr int qn = (q + 1) & 7;
+                const TinyCf& on = q < 7 ? o0 : o1;
+                uint32_t g = swz_from<qn>(on.geo);
+                g = q < 7 || more ? g : 0u;
+                const uint64_t Sn = (uint64_t(swz_from<qn>(uint32_t(on.S >> 32))) << 32) |
+                                    swz_from<qn>(uint32_t(on.S));
+                gq[(q + 1) & 1] = g;
+                load_entry(g, Sn, buf[(q + 1) & 1]);
+            }
+            const uint32_t geo = gq[q & 1];
+            const uint32_t K = tk_windows(geo);
+            const uint32_t el = (geo & 0x3FF) - tk_tail(geo) - 128 * (K - 1);
+            uint32_t acc = tiny_win_hash(lds, buf[q & 1][0], (geo >> 10) & 0xF,
+                                         K > 1 ? 128u : (K ? el : 0u), gl, g4);
+#pragma unroll
+            for (int k = 1; k < kTinyK; k++) {
+                if (__builtin_amdgcn_ballot_w64(uint32_t(k) < K)) {   // uniform
+                    const uint32_t e = uint32_t(k) + 1 == K ? el : 128u;
+                    const uint32_t R = tiny_win_hash(lds, buf[q & 1][k], 0, uint32_t(k) < K ? e : 0u, gl, g4);
+                    // X^e(acc) by lanes gl & 3 (byte gl & 3 at distance e - (gl & 3))
+                    const uint32_t kk = gl & 3;
+                    uint32_t X = tabv(e - kk, (acc >> (8 * kk)) & 0xFF);
+                    X ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(X), 0xB1, 0xF, 0xF, false));
+                    X ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(X), 0x4E, 0xF, 0xF, false));
+                    acc = uint32_t(k) < K ? (X ^ R) : acc;
+                }
+            }
+            mine = gl == uint32_t(q) ? acc : mine;
+        });
+        // own slot: the initial state X^(n - tail)(init) in steps of at most 128,
+        // then the tail bytewise
+        if (o0.ix != kNoIdx) {
+            const uint32_t n = (o0.geo >> 16) & 0x3FF, tail = tk_tail(o0.geo);
+            uint32_t v = o0.init, m = n - tail;
+            while (m > 128) {
+                const uint32_t st = m - 128 >= 4 ? 128u : m - 4;
+                v = xshift(v, st);
+                m -= st;
+            }
+            uint32_t R = mine ^ xshift(v, m);
+            for (uint32_t k = 3 - tail; k < 3; k++)   // bytes E - tail .. E - 1
+                R = tabv(1, (R ^ (tc >> (8 * k))) & 0xFF) ^ (R >> 8);
+            const uint32_t Rf = finalize ? ~R : R;
+            d.out[o0.ix] = Rf;
+            if (d.vstat && Rf != sc)
+                atomicAdd(&d.vstat[d.rec[o0.ix].x].bad_objects, 1u);
+        }
+        o0 = o1;
+        w1 = w2;
+        sc = sn;
+        tc = tn;
+    }
+}
+
 // Entries of two or more 128-byte steps (bins >= 2).  One octet (8 entries,
 // one per lane group) at a time:
 //   step 0 (head)          start mask and init injection, precomputed per octet;
@@ -1825,7 +2111,10 @@ template <bool kSmall>
 __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so, const uint8_t* lds,
                                             uint32_t blk, uint32_t nblk)
 {
-    constexpr int b0 = kSmall ? 2 : kSmallK + 1, b1 = kSmall ? kSmallK + 1 : kNB;
+    constexpr int kT = kTinyK > kSmallK ? kTinyK : kSmallK;
+    constexpr int b0 = kSmall ? (kTinyK > 1 ? kTinyK + 1 : 2) : kT + 1, b1 = kSmall ? kSmallK + 1 : kNB;
+    if (b0 >= b1)
+        return;
     const uint64_t* s_items = reinterpret_cast<const uint64_t*>(lds + kBinOff);   // kNB + 1
     const uint64_t* s_start = s_items + (kNB + 1);                                // kNB
     const uint32_t* s_cost = reinterpret_cast<const uint32_t*>(s_start + kNB);    // kNB
@@ -2249,7 +2538,10 @@ __global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc 
     };
 #if RAMCRC_TINY_CF
     RAMCRC_STAMP(0);
-    const bool tiny_ok = tiny_run_cf(d, so, lds, bad, blockIdx.x, gridDim.x);
+    const bool have_tk = kTinyK >= 2 && !so.bt->direct_n && so.bt->start[kTinyK + 1] != so.bt->start[2];
+    bool tiny_ok = tiny_run_cf(d, so, lds, bad, blockIdx.x, gridDim.x, have_tk);
+    if (tiny_ok && have_tk)
+        tiny_multi(d, so, lds, blockIdx.x, gridDim.x);
     RAMCRC_STAMP(1);
 #else
     const bool tiny_ok = tiny_run(d, so, lds, bad, blockIdx.x, gridDim.x);
@@ -2296,32 +2588,39 @@ __global__ __launch_bounds__(kThreads) void k_plan_count(BatchDesc d, Plan pl)
     __shared__ uint64_t wsum[kWavesPerGroup];
     if (plan_empty(pl))
         return;   // no large buffer: nothing reads local[] / group_pref[] of this launch
-    const uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
-    uint64_t c = 0;
-    if (i < entry_count<kMode>(d)) {   // local[] is still written for every i < d.n
-        uint64_t S, E;
-        buffer_range<kMode>(d, i, S, E);
-        c = is_large(E - S) ? chunk_count(S, E, d.cshift) : 0;
-    }
-    // exclusive scan over the workgroup: in-wave inclusive scan, then waves
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint64_t x = c;
+    // groups of kThreads entries, grid-stride (the grid is capped: a batch of
+    // tens of millions of records launches few workgroups when it has no
+    // large buffer and every one of them returns above)
+    const uint64_t n = entry_count<kMode>(d);
+    for (uint64_t grp = blockIdx.x; grp < pl.ngroups; grp += gridDim.x) {
+        const uint64_t i = grp * kThreads + threadIdx.x;
+        uint64_t c = 0;
+        if (i < n) {   // local[] is still written for every i < d.n
+            uint64_t S, E;
+            buffer_range<kMode>(d, i, S, E);
+            c = is_large(E - S) ? chunk_count(S, E, d.cshift) : 0;
+        }
+        // exclusive scan over the workgroup: in-wave inclusive scan, then waves
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        uint64_t x = c;
 #pragma unroll
-    for (int s = 1; s < 64; s <<= 1) {
-        const uint64_t y = __shfl_up(x, s, kWaveSize);
-        if (lane >= s)
-            x += y;
+        for (int s = 1; s < 64; s <<= 1) {
+            const uint64_t y = __shfl_up(x, s, kWaveSize);
+            if (lane >= s)
+                x += y;
+        }
+        if (lane == 63)
+            wsum[w] = x;
+        __syncthreads();
+        uint64_t before = 0;
+        for (int j = 0; j < w; j++)
+            before += wsum[j];
+        if (i < d.n)
+            pl.local[i] = before + x - c;
+        if (threadIdx.x == kThreads - 1)
+            pl.group_pref[grp] = before + x;   // group total, scanned by k_plan_scan
+        __syncthreads();   // wsum is reused by the next group
     }
-    if (lane == 63)
-        wsum[w] = x;
-    __syncthreads();
-    uint64_t before = 0;
-    for (int j = 0; j < w; j++)
-        before += wsum[j];
-    if (i < d.n)
-        pl.local[i] = before + x - c;
-    if (threadIdx.x == kThreads - 1)
-        pl.group_pref[blockIdx.x] = before + x;   // group total, scanned by k_plan_scan
 }
 
 __global__ __launch_bounds__(kThreads) void k_plan_scan(Plan pl)
@@ -2701,7 +3000,9 @@ int launch_planned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s)
         return rc;
     Plan pl = make_plan(c, d.n);
     pl.nlarge = &so.bt->ctr[so.par].nlarge;
-    hipLaunchKernelGGL(k_plan_count<kMode>, dim3(pl.ngroups), dim3(kThreads), 0, s, d, pl);
+    const uint64_t gcap = uint64_t(4) * c->ncu;
+    hipLaunchKernelGGL(k_plan_count<kMode>, dim3(uint32_t(pl.ngroups < gcap ? pl.ngroups : gcap)),
+                       dim3(kThreads), 0, s, d, pl);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(kThreads), 0, s, pl);
     HIPCHK(hipGetLastError());
@@ -2710,9 +3011,10 @@ int launch_planned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s)
         t.launch(k_chunks<kMode>, dim3(c->ncu), dim3(kThreads), d, pl, uint64_t(0));
     }
     HIPCHK(hipGetLastError());
+    const uint64_t cw = (d.n + 255) / 256, ccap = uint64_t(16) * c->ncu;
     if (d.n > kWideCombineMin)
-        hipLaunchKernelGGL((k_combine<kMode, true>), dim3((d.n + 255) / 256), dim3(256), 0, s, d, pl,
-                           uint64_t(0));
+        hipLaunchKernelGGL((k_combine<kMode, true>), dim3(uint32_t(cw < ccap ? cw : ccap)), dim3(256), 0, s,
+                           d, pl, uint64_t(0));
     else
         hipLaunchKernelGGL((k_combine<kMode, false>), dim3((d.n + 3) / 4), dim3(256), 0, s, d, pl,
                            uint64_t(0));
