@@ -868,10 +868,14 @@ constexpr int kSmallK = RAMCRC_SMALLK;     // bins 2..kSmallK: octets loaded one
 #ifndef RAMCRC_TINY_K
 #define RAMCRC_TINY_K 4
 #endif
+#ifndef RAMCRC_TINY_WR
+#define RAMCRC_TINY_WR 1   // tiny phases: window-relative table, one v_perm per address, owner un-shift
+#endif
 // bins 2 .. kTinyK (entries of 2 .. kTinyK windows, e.g. objects of 129 ..
 // ~500 B): the multi-window tiny phase (tiny_run_cf<true>); 1 = off (the short bins)
 constexpr int kTinyK = RAMCRC_TINY_K;
 static_assert(kTinyK >= 1 && kTinyK <= 4, "tiny windows: e_tot fits 10 bits");
+static_assert(kTinyK == 1 || RAMCRC_TINY_WR, "tiny_multi uses the window-relative table");
 #ifndef RAMCRC_ENT_NT
 #define RAMCRC_ENT_NT 1
 #endif
@@ -1688,24 +1692,72 @@ __device__ __forceinline__ uint32_t tk_windows(uint32_t geo)
     return ((geo & 0x3FFu) - tk_tail(geo) + 127u) >> 7;
 }
 
-// The group's sum over one window's bytes in [sa, e), each byte b at window
-// offset o as X^(e - o)(b) (all 8 lanes of the group get it).
-__device__ __forceinline__ uint32_t tiny_win_hash(const uint8_t* lds, const u32x4& wv, uint32_t sa,
-                                                  uint32_t e, uint32_t gl, uint32_t g4)
+// RAMCRC_TINY_WR: the tiny phases' LDS holds X^(128 - q)(b) for window
+// position q at ((q >> 6) << 16) | (b << 8) | ((q & 63) << 2) -- the data byte
+// is address byte 1, so one v_perm forms an address from a per-lane constant
+// -- and X^-128 (4 x 256 words) after it.  A window's bytes are summed at their
+// distance from the window's end, whatever the entry; the owner lane moves its
+// entry's sum to the entry end with X^e(X^-128(.)) (8 lookups per slot instead
+// of per-window row arithmetic in every lane).  Masked bytes are 0, and
+// X^m(0) = 0.
+constexpr uint32_t kTwInvOff = 131072;
+constexpr uint32_t kLdsTinyWr = kTwInvOff + 4096;
+static_assert(kLdsTinyWr <= kLdsEntries, "k_entries' LDS holds the tiny phases' tables");
+
+__device__ __forceinline__ uint32_t tw_addr(uint32_t q, uint32_t b)
 {
-    const uint32_t c = (e + g4) & 3;                  // byte rotation of this group
-    const uint32_t bb = 512 - 4 * e + 16 * gl;        // 4 (128 - e + 4 u): row of offset 4 u
-    const uint32_t rot = __builtin_amdgcn_alignbyte(0x0C080400u, 0x0C080400u, c);
-    // byte k of the rotated dword sits at window offset 4 u + ((k + c) & 3)
-    // (row bits below 512 for every byte of the entry; a masked byte's
-    // column 255 is zero at every row, so OR-ing its larger row is safe)
-    uint32_t pk[4];
+    return ((q >> 6) << 16) | (b << 8) | ((q & 63) << 2);
+}
+
+__device__ __forceinline__ void tiny_fill_wr(uint8_t* lds)
+{
+    // 8192 chunks of 16 B, chunk (h, b, c) = words 128 (255 - b) + 64 h + 4 c .. of
+    // g_tab.post (X^m(b) at 128 (255 - b) + 128 - m), then the X^-128 table
+    constexpr uint32_t kPos = 8192, kAll = kPos + 256;
+    constexpr uint32_t kPer = (kAll + kEntWaves * kWaveSize - 1) / (kEntWaves * kWaveSize);
+    const uint4* post = reinterpret_cast<const uint4*>(g_tab.post);
+    const uint4* inv = reinterpret_cast<const uint4*>(&g_tab.xinv128);
+    uint4 v[kPer];
 #pragma unroll
-    for (int k = 0; k < 4; k++)
-        pk[k] = bb + ((rot >> (8 * k)) & 0xFF);
-    // tail: dword j keeps its bytes before E, clamp(e - 32 j - 4 u, 0, 4)
+    for (uint32_t j = 0; j < kPer; j++) {
+        const uint32_t i = threadIdx.x + j * (kEntWaves * kWaveSize);
+        if (i < kPos) {
+            const uint32_t h = i >> 12, b = (i >> 4) & 255, c = i & 15;
+            v[j] = post[(128 * (255 - b) + 64 * h) / 4 + c];
+        } else if (i < kAll) {
+            v[j] = inv[i - kPos];
+        }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+        const uint32_t i = threadIdx.x + j * (kEntWaves * kWaveSize);
+        if (i < kAll)
+            *reinterpret_cast<uint4*>(lds + 16 * i) = v[j];
+    }
+}
+
+// Per-lane address constants: byte k of a rotated dword (window position
+// 32 j + 4 u + ((k + g4) & 3)) of dword pair j >> 1; + 128 for odd j.
+struct TwRows {
+    uint32_t lr[2][4];
+    __device__ TwRows(uint32_t gl, uint32_t g4)
+    {
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                lr[h][k] = (uint32_t(h) << 16) | (16 * gl + 4 * ((uint32_t(k) + g4) & 3));
+    }
+};
+
+// The group's sum over one window's bytes in [sa, e), byte b at position o
+// as X^(128 - o)(b) (relative to the window's end; all 8 lanes get it).
+__device__ __forceinline__ uint32_t tiny_win_wr(const uint8_t* lds, const u32x4& wv, uint32_t sa,
+                                                uint32_t e, const TwRows& rw, uint32_t gl, uint32_t g4)
+{
+    // tail: dword j keeps its bytes before e, clamp(e - 32 j - 4 u, 0, 4)
     const int z = 32 - 8 * int(e) + 32 * int(gl);   // bits to drop from dword 0's top
-    // head: window bytes before S lie in dword 0 of lanes 0-3
+    // head: window bytes before sa lie in dword 0 of lanes 0-3
     const uint32_t hd = uint32_t(min(max(8 * (int(sa) - 4 * int(gl)), 0), 32));
     const uint32_t ws[4] = {wv.x, wv.y, wv.z, wv.w};
     uint32_t v[16];
@@ -1715,12 +1767,13 @@ __device__ __forceinline__ uint32_t tiny_win_hash(const uint8_t* lds, const u32x
         uint32_t keep = uint32_t(uint64_t(0xFFFFFFFFu) >> sh);
         if (j == 0)
             keep &= uint32_t(~uint64_t(0) << hd);
-        const uint32_t xb = ~(ws[j] & keep);          // masked bytes -> column 255
-        const uint32_t xr = __builtin_amdgcn_alignbyte(xb, xb, c);
+        const uint32_t xb = ws[j] & keep;
+        const uint32_t xr = __builtin_amdgcn_alignbyte(xb, xb, g4);   // conflict-free banks
 #pragma unroll
         for (int k = 0; k < 4; k++)
             v[4 * j + k] = *reinterpret_cast<const uint32_t*>(
-                lds + ((((xr >> (8 * k)) & 0xFF) << 9) | pk[k]) + 128 * j);
+                lds + __builtin_amdgcn_perm(xr, rw.lr[j >> 1][k], 0x0C020000u | ((4u + uint32_t(k)) << 8)) +
+                128 * (j & 1));
     }
     const uint32_t t0 = xor3(v[0], v[1], v[2]), t1 = xor3(v[3], v[4], v[5]);
     const uint32_t t2 = xor3(v[6], v[7], v[8]), t3 = xor3(v[9], v[10], v[11]);
@@ -1732,6 +1785,22 @@ __device__ __forceinline__ uint32_t tiny_win_hash(const uint8_t* lds, const u32x
     return R;
 }
 
+// X^m(v) for 4 <= m <= 128 (byte k at distance m - k), and X^-128(v)
+__device__ __forceinline__ uint32_t tw_shift(const uint8_t* lds, uint32_t v, uint32_t m)
+{
+    auto t = [&](uint32_t q, uint32_t b) { return *reinterpret_cast<const uint32_t*>(lds + tw_addr(q, b)); };
+    return xor3(t(128 - m, v & 0xFF), t(129 - m, (v >> 8) & 0xFF), t(130 - m, (v >> 16) & 0xFF)) ^
+           t(131 - m, v >> 24);
+}
+
+__device__ __forceinline__ uint32_t tw_inv128(const uint8_t* lds, uint32_t v)
+{
+    auto t = [&](uint32_t k, uint32_t b) {
+        return *reinterpret_cast<const uint32_t*>(lds + kTwInvOff + 4 * (256 * k + b));
+    };
+    return xor3(t(0, v & 0xFF), t(1, (v >> 8) & 0xFF), t(2, (v >> 16) & 0xFF)) ^ t(3, v >> 24);
+}
+
 __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so, uint8_t* lds,
                                             bool bad, uint32_t blk, uint32_t nblk, bool need_table)
 {
@@ -1740,7 +1809,7 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
         // no entry of at most one window (uniform: every wave exits); the
         // multi-window phase still needs the table
         if (need_table) {
-            fill_plain(lds, 0, g_tab.post, 256 * 128 + 128);
+            tiny_fill_wr(lds);
             return !__syncthreads_or(bad);
         }
         return true;
@@ -1836,14 +1905,21 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
             w[q] = v;
         });
     };
+#if !RAMCRC_TINY_WR
     // X^m(b) in the column-major table
     auto tabv = [&](uint32_t m, uint32_t b) -> uint32_t {
         return *reinterpret_cast<const uint32_t*>(lds + 512 * (255 - b) + 4 * (128 - m));
     };
+#endif
 
     uint64_t r = wave;
     TinyOwn o0 = load_own(r), o1 = load_own(r + nwaves);
+#if RAMCRC_TINY_WR
+    tiny_fill_wr(lds);
+    const TwRows rw(gl, g4);
+#else
     fill_plain(lds, 0, g_tab.post, 256 * 128 + 128);
+#endif
     if (__syncthreads_or(bad))
         return false;
     RAMCRC_STAMP(5);
@@ -1858,6 +1934,15 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
         if (r + nwaves < rounds)
             issue(o1, wn, gn, sn);
         uint32_t mine = 0;
+#if RAMCRC_TINY_WR
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const uint32_t sa = (gc[q] >> 8) & 0xF;
+            const uint32_t e = sa + (gc[q] & 0xFF);           // window-relative end, <= 128
+            const uint32_t R = tiny_win_wr(lds, wc[q], sa, e, rw, gl, g4);
+            mine = gl == uint32_t(q) ? R : mine;
+        }
+#else
 #pragma unroll
         for (int q = 0; q < 8; q++) {
             const uint32_t sa = (gc[q] >> 8) & 0xF;
@@ -1900,10 +1985,24 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
             R ^= uint32_t(__builtin_amdgcn_ds_swizzle(int(R), 0x1F | (4 << 10)));           // lane ^ 4
             mine = gl == uint32_t(q) ? R : mine;
         }
+#endif
         // own slot: the initial state (byte k at distance len - k), or bytewise
         if (o0.ix != kNoIdx) {
             uint32_t R;
             const uint32_t n = (o0.geo >> 16) & 0xFF;   // the entry's length
+#if RAMCRC_TINY_WR
+            if (n >= 4) {
+                // the window sum moved from the window's end to the entry's end,
+                // e = S - A + n >= 4 bytes into the window
+                const uint32_t e = ((o0.geo >> 8) & 0xF) + n;
+                R = tw_shift(lds, tw_inv128(lds, mine), e) ^ tw_shift(lds, o0.init, n);
+            } else {
+                R = o0.init;
+                for (uint32_t k = 0; k < n; k++)
+                    R = *reinterpret_cast<const uint32_t*>(
+                            lds + tw_addr(127, (R ^ *(const gu8*)(o0.S + k)) & 0xFF)) ^ (R >> 8);
+            }
+#else
             if (n >= 4) {
                 const uint32_t in = o0.init;
                 R = mine ^ xor3(tabv(n, in & 0xFF), tabv(n - 1, (in >> 8) & 0xFF),
@@ -1914,6 +2013,7 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
                 for (uint32_t k = 0; k < n; k++)
                     R = tabv(1, (R ^ *(const gu8*)(o0.S + k)) & 0xFF) ^ (R >> 8);
             }
+#endif
             const uint32_t Rf = finalize ? ~R : R;
             d.out[o0.ix] = Rf;
             if (d.vstat && Rf != sc)
@@ -1989,13 +2089,7 @@ __device__ __forceinline__ void tiny_multi(const BatchDesc& d, const Sorted& so,
         const uint32_t w1 = *reinterpret_cast<g32*>(b & ~uint64_t(3));
         tw = __builtin_amdgcn_alignbyte(w1, w0, uint32_t(a) & 3);   // bytes E - 3, E - 2, E - 1
     };
-    auto tabv = [&](uint32_t m, uint32_t b) -> uint32_t {
-        return *reinterpret_cast<const uint32_t*>(lds + 512 * (255 - b) + 4 * (128 - m));
-    };
-    auto xshift = [&](uint32_t v, uint32_t m) -> uint32_t {   // X^m(v), 4 <= m <= 128
-        return xor3(tabv(m, v & 0xFF), tabv(m - 1, (v >> 8) & 0xFF), tabv(m - 2, (v >> 16) & 0xFF)) ^
-               tabv(m - 3, v >> 24);
-    };
+    const TwRows rw(gl, g4);
     // the windows of the entry (geo, S) into w: window k is [A + 128 k, + 128);
     // a dword at or past the window's last entry byte reads that byte's dword
     auto load_entry = [&](uint32_t geo, uint64_t S, u32x4 (&w)[kTinyK]) {
@@ -2049,16 +2143,18 @@ __device__ __forceinline__ void tiny_multi(const BatchDesc& d, const Sorted& so,
             const uint32_t geo = gq[q & 1];
             const uint32_t K = tk_windows(geo);
             const uint32_t el = (geo & 0x3FF) - tk_tail(geo) - 128 * (K - 1);
-            uint32_t acc = tiny_win_hash(lds, buf[q & 1][0], (geo >> 10) & 0xF,
-                                         K > 1 ? 128u : (K ? el : 0u), gl, g4);
+            // window sums at their distance from their window's end; Horner with
+            // X^128 between windows: acc is relative to the last window's end
+            uint32_t acc = tiny_win_wr(lds, buf[q & 1][0], (geo >> 10) & 0xF,
+                                       K > 1 ? 128u : (K ? el : 0u), rw, gl, g4);
 #pragma unroll
             for (int k = 1; k < kTinyK; k++) {
                 if (__builtin_amdgcn_ballot_w64(uint32_t(k) < K)) {   // uniform
                     const uint32_t e = uint32_t(k) + 1 == K ? el : 128u;
-                    const uint32_t R = tiny_win_hash(lds, buf[q & 1][k], 0, uint32_t(k) < K ? e : 0u, gl, g4);
-                    // X^e(acc) by lanes gl & 3 (byte gl & 3 at distance e - (gl & 3))
+                    const uint32_t R = tiny_win_wr(lds, buf[q & 1][k], 0, uint32_t(k) < K ? e : 0u, rw, gl, g4);
+                    // X^128(acc) by lanes gl & 3 (byte gl & 3 at distance 128 - (gl & 3))
                     const uint32_t kk = gl & 3;
-                    uint32_t X = tabv(e - kk, (acc >> (8 * kk)) & 0xFF);
+                    uint32_t X = *reinterpret_cast<const uint32_t*>(lds + tw_addr(kk, (acc >> (8 * kk)) & 0xFF));
                     X ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(X), 0xB1, 0xF, 0xF, false));
                     X ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(X), 0x4E, 0xF, 0xF, false));
                     acc = uint32_t(k) < K ? (X ^ R) : acc;
@@ -2070,15 +2166,19 @@ __device__ __forceinline__ void tiny_multi(const BatchDesc& d, const Sorted& so,
         // then the tail bytewise
         if (o0.ix != kNoIdx) {
             const uint32_t n = (o0.geo >> 16) & 0x3FF, tail = tk_tail(o0.geo);
+            const uint32_t K = tk_windows(o0.geo);
+            const uint32_t el = (o0.geo & 0x3FF) - tail - 128 * (K - 1);   // >= 4
             uint32_t v = o0.init, m = n - tail;
             while (m > 128) {
                 const uint32_t st = m - 128 >= 4 ? 128u : m - 4;
-                v = xshift(v, st);
+                v = tw_shift(lds, v, st);
                 m -= st;
             }
-            uint32_t R = mine ^ xshift(v, m);
+            // the windows' sum moved from the last window's end to E - tail
+            uint32_t R = tw_shift(lds, tw_inv128(lds, mine), el) ^ tw_shift(lds, v, m);
             for (uint32_t k = 3 - tail; k < 3; k++)   // bytes E - tail .. E - 1
-                R = tabv(1, (R ^ (tc >> (8 * k))) & 0xFF) ^ (R >> 8);
+                R = *reinterpret_cast<const uint32_t*>(lds + tw_addr(127, (R ^ (tc >> (8 * k))) & 0xFF)) ^
+                    (R >> 8);
             const uint32_t Rf = finalize ? ~R : R;
             d.out[o0.ix] = Rf;
             if (d.vstat && Rf != sc)
