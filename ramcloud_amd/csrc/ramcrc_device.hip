@@ -892,6 +892,9 @@ constexpr int kPU = RAMCRC_PU;             // ping-pong depth (pipelined bins)
 #ifndef RAMCRC_TINY_SAFE
 #define RAMCRC_TINY_SAFE 1    // tiny_run_cf: unclamped window loads when every window of a q is page-safe
 #endif
+#ifndef RAMCRC_TINY_LD4
+#define RAMCRC_TINY_LD4 0   // A/B only: tiny windows as one 16-byte load per lane, wrong CRCs
+#endif
 #ifndef RAMCRC_TINY_PROBE
 #define RAMCRC_TINY_PROBE 0  // A/B only: conflict-free lookup addresses, wrong CRCs
 #endif
@@ -1890,10 +1893,14 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
             u32x4 v;
             if (RAMCRC_TINY_SAFE && __builtin_amdgcn_ballot_w64(!((geo[q] >> 12) & 1)) == 0) {
                 // every window of this q is page-safe: plain loads, immediate offsets
+#if RAMCRC_TINY_LD4
+                v = load16(A + 16 * gl);   // A/B probe only (wrong CRCs): one 16-byte load per lane
+#else
                 v.x = *reinterpret_cast<g32*>(au);
                 v.y = *reinterpret_cast<g32*>(au + 32);
                 v.z = *reinterpret_cast<g32*>(au + 64);
                 v.w = *reinterpret_cast<g32*>(au + 96);
+#endif
             } else {
                 const uint32_t e = ((geo[q] >> 8) & 0xF) + (geo[q] & 0xFF);   // E - A (0: empty)
                 const int el = (max(int(e) - 1, 0) & ~3) - int(4 * gl);   // last dword, from 4 u
