@@ -207,7 +207,8 @@ typedef struct ramcrc_seg_status {
  * at d_base + i*seg_stride, each of seg_capacity bytes (a multiple of 16; the
  * reference's segletBlocks.size() * segletSize), against d_certs[i].  The
  * length-prefixed entries are walked in parallel over parts of every segment
- * (64 KiB by default; see RAMCRC_OPT_SERIAL_WALK, RAMCRC_OPT_WALK_PART_SHIFT).  Writes d_status[i] and one
+ * (about 64 entries per part, 64 KiB .. 1 MiB, chosen per batch on the device from
+ * the entry density; see RAMCRC_OPT_SERIAL_WALK, RAMCRC_OPT_WALK_PART_SHIFT).  Writes d_status[i] and one
  * ramcrc_seg_entry per complete entry to d_entries (up to entries_cap; the
  * order across segments is unspecified, within a segment it is increasing).  *d_n_entries (device) receives the
  * number of entries walked (may exceed entries_cap: see TABLE_FULL).
@@ -435,10 +436,11 @@ int ramcrc_assemble_objects_host(ramcrc_ctx* ctx, void* const* objs, const uint6
  *                           identical results. */
 #define RAMCRC_OPT_SERIAL_WALK 1
 /*   RAMCRC_OPT_WALK_PART_SHIFT  log2 of the parallel walk's part size, 13..20
- *                           (8 KiB .. 1 MiB); 0: the default, 64 KiB.
+ *                           (8 KiB .. 1 MiB), forced for every batch; 0: the
+ *                           default, chosen per batch from the entry density
+ *                           (about 64 entries per part, 64 KiB .. 1 MiB).
  *                           Results are identical for every part size (the
- *                           parity tests run several); smaller parts measured
- *                           no faster even on segments of 100-byte entries. */
+ *                           parity tests run several). */
 #define RAMCRC_OPT_WALK_PART_SHIFT 2
 /*   RAMCRC_OPT_TEST_FAIL_AFTER_COUNT  test hook: the next `value` small-entry
  *                           launch sequences return RAMCRC_EHIP right after

@@ -515,6 +515,21 @@ __device__ __forceinline__ uint64_t entry_count(const BatchDesc& d)
     return d.n;
 }
 
+// Header bytes a record of `type` must hold to be checked; 0 = not checked.
+__device__ __forceinline__ uint32_t replay_header_bytes(uint32_t type)
+{
+    switch (type) {
+    case RAMCRC_LOG_ENTRY_TYPE_OBJ: return kObjHeaderBytes;
+    case RAMCRC_LOG_ENTRY_TYPE_OBJTOMB: return kTombHeaderBytes;
+    case RAMCRC_LOG_ENTRY_TYPE_SAFEVERSION: return kSafeVersionBytes;
+    case RAMCRC_LOG_ENTRY_TYPE_PREP: return kPrepHeaderBytes + kObjHeaderBytes;
+    case RAMCRC_LOG_ENTRY_TYPE_PREPTOMB: return kPrepTombBytes;
+    case RAMCRC_LOG_ENTRY_TYPE_TXDECISION: return kTxDecisionHeaderBytes;
+    case RAMCRC_LOG_ENTRY_TYPE_TXPLIST: return kTxPlistHeaderBytes;
+    default: return 0;
+    }
+}
+
 // [S, E) of buffer i; false for an inactive record (then S == E).
 template <int kMode>
 __device__ __forceinline__ bool buffer_range(const BatchDesc& d, uint64_t i, uint64_t& S,
@@ -685,6 +700,17 @@ __device__ __forceinline__ uint32_t scan_chunk(const uint8_t* lds, const RepOp& 
     }
     return z;
 }
+
+// A record k_obj_compare has work for: a checked type that is not a readable
+// object below the large-buffer split (those are compared beside the scan).
+__device__ __forceinline__ bool replay_other(const u32x4& r)
+{
+    const uint32_t type = r.w & 0x3f;
+    const uint32_t hdr = replay_header_bytes(type);
+    const bool readable = r.z >= hdr && !(r.w & kRecOverlong);
+    return hdr != 0 && !(type == RAMCRC_LOG_ENTRY_TYPE_OBJ && readable && !is_large(uint64_t(r.z) - 4));
+}
+
 
 // Locate (entry, chunk) for global chunk index g in general mode.
 __device__ __forceinline__ void plan_locate(const Plan& pl, uint64_t n, uint64_t g, uint64_t& entry,
@@ -983,6 +1009,8 @@ struct BinCounters {
     uint32_t hist[kNB];       // entry counts
     uint32_t nlarge;          // large buffers the count pass left to k_chunks (skip_large)
     uint32_t ninact;          // inactive records (records mode: not checked here)
+    uint32_t nother;          // records mode: records k_obj_compare has work for (replay_other)
+    uint32_t pad_;
 };
 
 struct BinTable {
@@ -1086,7 +1114,7 @@ template <int kMode>
 __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, int skip_large)
 {
     __shared__ uint32_t h[kNB];
-    __shared__ uint32_t nlarge, ninact;
+    __shared__ uint32_t nlarge, ninact, nother;
     BinCounters& ctr = so.bt->ctr[so.par];
     if (blockIdx.x == 0) {
         // the next sequence's counters (see BinCounters)
@@ -1098,6 +1126,7 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
         if (threadIdx.x == 0) {
             nx.nlarge = 0;
             nx.ninact = 0;
+            nx.nother = 0;
         }
     }
     for (int t = threadIdx.x; t < kNB; t += blockDim.x)
@@ -1105,6 +1134,7 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
     if (threadIdx.x == 0) {
         nlarge = 0;
         ninact = 0;
+        nother = 0;
     }
     __syncthreads();
     const uint64_t tile = uint64_t(blockDim.x) * kBinPer;
@@ -1118,12 +1148,16 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
             S[q] = E[q] = 0;
             act[q] = i < n && buffer_range<kMode>(d, i, S[q], E[q]);
         }
-        uint32_t big = 0, inact = 0;
+        uint32_t big = 0, inact = 0, other = 0;
 #pragma unroll
         for (int q = 0; q < kBinPer; q++) {
             const bool large = skip_large && is_large(E[q] - S[q]);
             big += act[q] && large;
             inact += !act[q] && base + uint64_t(q) * blockDim.x + threadIdx.x < n;
+            if constexpr (kMode == kRecords) {
+                const uint64_t i = base + uint64_t(q) * blockDim.x + threadIdx.x;
+                other += i < n && replay_other(d.rec[i]);
+            }
             const bool active = act[q] && !large;
             const int b = active ? bin_of(S[q], E[q]) : 0;
             uint32_t unused;
@@ -1137,6 +1171,10 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
             if (inact)
                 atomicAdd(&ninact, inact);
         }
+        if (kMode == kRecords && __ballot(other != 0)) {
+            if (other)
+                atomicAdd(&nother, other);
+        }
     }
     __syncthreads();
     for (int t = threadIdx.x; t < kNB; t += blockDim.x)
@@ -1146,6 +1184,8 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
         atomicAdd(&ctr.nlarge, nlarge);
     if (threadIdx.x == 0 && ninact)
         atomicAdd(&ctr.ninact, ninact);
+    if (threadIdx.x == 0 && nother)
+        atomicAdd(&ctr.nother, nother);
 }
 
 // Bin layout from the histogram, computed by every k_bin_scatter workgroup
@@ -3099,12 +3139,14 @@ int launch_binned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_lar
 }
 
 template <int kMode>
-int launch_planned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s)
+int launch_planned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, const uint32_t** nother = nullptr)
 {
     Sorted so;
     int rc = bin_begin<kMode>(c, d, s, 1, &so);
     if (rc)
         return rc;
+    if (nother)
+        *nother = &so.bt->ctr[so.par].nother;
     Plan pl = make_plan(c, d.n);
     pl.nlarge = &so.bt->ctr[so.par].nlarge;
     const uint64_t gcap = uint64_t(4) * c->ncu;
@@ -4874,31 +4916,30 @@ __device__ __forceinline__ uint32_t le32_g(const gu8* p)
     return uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
 }
 
-// Header bytes a record of `type` must hold to be checked; 0 = not checked.
-__device__ __forceinline__ uint32_t replay_header_bytes(uint32_t type)
-{
-    switch (type) {
-    case RAMCRC_LOG_ENTRY_TYPE_OBJ: return kObjHeaderBytes;
-    case RAMCRC_LOG_ENTRY_TYPE_OBJTOMB: return kTombHeaderBytes;
-    case RAMCRC_LOG_ENTRY_TYPE_SAFEVERSION: return kSafeVersionBytes;
-    case RAMCRC_LOG_ENTRY_TYPE_PREP: return kPrepHeaderBytes + kObjHeaderBytes;
-    case RAMCRC_LOG_ENTRY_TYPE_PREPTOMB: return kPrepTombBytes;
-    case RAMCRC_LOG_ENTRY_TYPE_TXDECISION: return kTxDecisionHeaderBytes;
-    case RAMCRC_LOG_ENTRY_TYPE_TXPLIST: return kTxPlistHeaderBytes;
-    default: return 0;
-    }
-}
 
 // skip_objs: every readable object was checked by the ordered scan
 // (k_stream<true>); bad_seq (nullable) == seq: that scan was refused, and
 // nothing is checked here either.
+// nother (nullable): the binning count of records this kernel has work for
+// (replay_other); 0 ends the launch at once.  Grid-stride over the records.
+__device__ __forceinline__ void obj_compare_one(const BatchDesc& d, ramcrc_seg_status* status,
+                                                int skip_objs, uint64_t i);
+
 __global__ __launch_bounds__(256) void k_obj_compare(BatchDesc d, ramcrc_seg_status* status,
                                                      int skip_objs, const uint32_t* bad_seq,
-                                                     uint32_t seq)
+                                                     uint32_t seq, const uint32_t* nother)
 {
-    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= entry_count<kRecords>(d) || (bad_seq && *bad_seq == seq))
+    if ((bad_seq && *bad_seq == seq) || (nother && *nother == 0))
         return;
+    const uint64_t n = entry_count<kRecords>(d);
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+         i += uint64_t(gridDim.x) * blockDim.x)
+        obj_compare_one(d, status, skip_objs, i);
+}
+
+__device__ __forceinline__ void obj_compare_one(const BatchDesc& d, ramcrc_seg_status* status,
+                                                int skip_objs, uint64_t i)
+{
     const u32x4 r = d.rec[i];
     const uint32_t type = r.w & 0x3f;
     const uint32_t hdr = replay_header_bytes(type);
@@ -5767,12 +5808,14 @@ int ramcrc_verify_objects_device(ramcrc_ctx* c, const void* d_base, uint64_t seg
     d.seg_status = reinterpret_cast<const u32x4*>(d_status);
     d.out = d_obj_crc;
     d.flags = RAMCRC_FINALIZE;
-    rc = launch_planned<kRecords>(c, d, s);
+    const uint32_t* nother = nullptr;
+    rc = launch_planned<kRecords>(c, d, s, &nother);
     if (rc)
         return rc;
-    const uint64_t grid = (entries_cap + 255) / 256;
+    uint64_t grid = (entries_cap + 255) / 256;
+    grid = grid < uint64_t(16) * c->ncu ? grid : uint64_t(16) * c->ncu;
     hipLaunchKernelGGL(k_obj_compare, dim3(grid), dim3(256), 0, s, d, d_status, 0,
-                       static_cast<const uint32_t*>(nullptr), 0u);
+                       static_cast<const uint32_t*>(nullptr), 0u, nother);
     HIPCHK(hipGetLastError());
     return RAMCRC_OK;
 }
@@ -5810,7 +5853,8 @@ int ramcrc_verify_objects_ordered_device(ramcrc_ctx* c, const void* d_base, uint
     // compare would read object CRCs that were never written)
     const uint64_t grid = (entries_cap + 255) / 256;
     hipLaunchKernelGGL(k_obj_compare, dim3(grid), dim3(256), 0, s, d, d_status, 1,
-                       static_cast<const uint32_t*>(c->stream_bad), c->stream_seq);
+                       static_cast<const uint32_t*>(c->stream_bad), c->stream_seq,
+                       static_cast<const uint32_t*>(nullptr));
     HIPCHK(hipGetLastError());
     return RAMCRC_OK;
 }

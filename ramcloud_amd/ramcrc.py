@@ -290,7 +290,8 @@ class Context:
         _check(lib().ramcrc_ctx_set_option(self._h, 1, 1 if enable else 0), "ramcrc_ctx_set_option")
 
     def set_walk_part_shift(self, shift):
-        """log2 of the parallel walk's part size, 13..20; 0 = the default 64 KiB
+        """log2 of the parallel walk's part size, 13..20, forced for every
+        batch; 0 = the default, chosen per batch from the entry density
         (RAMCRC_OPT_WALK_PART_SHIFT)."""
         _check(lib().ramcrc_ctx_set_option(self._h, 2, int(shift)), "ramcrc_ctx_set_option")
 

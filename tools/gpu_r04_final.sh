@@ -1,0 +1,24 @@
+# Round 4 final: GPU suite, smoke, every bench line on the final tree, kernel
+# traces of the headline and the config-3 / replay workloads.
+set -o pipefail
+OUT=gpurun_out/${1:-r04/final}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests -m gpu > "$OUT/pytest_gpu.log" 2>&1 || exit 1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$OUT/smoke.log" 2>&1 || exit 1
+timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 1
+timeout -k 10 300 python bench.py --config recovery > "$OUT/recovery.json" 2> "$OUT/recovery.err" || exit 1
+for sz in 0 100 1024 4096; do
+  timeout -k 10 200 python bench.py --config entries --entry-size $sz > "$OUT/c3_$sz.json" 2> "$OUT/c3_$sz.err" || exit 1
+done
+timeout -k 10 200 python bench.py --config append > "$OUT/append.json" 2> "$OUT/append.err" || exit 1
+timeout -k 10 300 python bench.py --config stream > "$OUT/stream.json" 2> "$OUT/stream.err" || exit 1
+for v in 64 128 256 512 1024 2048 8192; do
+  timeout -k 10 200 python bench.py --config replay --value-len $v --no-cpu-baseline > "$OUT/replay_$v.json" 2> "$OUT/replay_$v.err" || exit 1
+done
+timeout -k 10 200 python bench.py --config replay > "$OUT/replay.json" 2> "$OUT/replay.err" || exit 1
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o c2 -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline > "$OUT/prof_c2.json" 2> "$OUT/prof_c2.err" || exit 1
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o c3 -- python bench.py --config entries --steps 10 --no-cpu-baseline > "$OUT/prof_c3.json" 2> "$OUT/prof_c3.err" || exit 1
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o c3_100 -- python bench.py --config entries --entry-size 100 --steps 10 --no-cpu-baseline > "$OUT/prof_c3_100.json" 2> "$OUT/prof_c3_100.err" || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o replay -- python bench.py --config replay --steps 10 --no-cpu-baseline > "$OUT/prof_replay.json" 2> "$OUT/prof_replay.err" || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o replay64 -- python bench.py --config replay --value-len 64 --steps 10 --no-cpu-baseline > "$OUT/prof_replay64.json" 2> "$OUT/prof_replay64.err" || exit 1
