@@ -918,6 +918,9 @@ constexpr int kPU = RAMCRC_PU;             // ping-pong depth (pipelined bins)
 #ifndef RAMCRC_TINY_SAFE
 #define RAMCRC_TINY_SAFE 1    // tiny_run_cf: unclamped window loads when every window of a q is page-safe
 #endif
+#ifndef RAMCRC_TINY_LD16
+#define RAMCRC_TINY_LD16 0   // tiny phases: one 16-byte load per lane per window (layout above)
+#endif
 #ifndef RAMCRC_TINY_LD4
 #define RAMCRC_TINY_LD4 0   // A/B only: tiny windows as one 16-byte load per lane, wrong CRCs
 #endif
@@ -1747,11 +1750,57 @@ constexpr uint32_t kTwInvOff = 131072;
 constexpr uint32_t kLdsTinyWr = kTwInvOff + 4096;
 static_assert(kLdsTinyWr <= kLdsEntries, "k_entries' LDS holds the tiny phases' tables");
 
+#if RAMCRC_TINY_LD16
+// RAMCRC_TINY_LD16: position q = 4 r + k at ((k >> 1) << 16) | (b << 8) |
+// ((k & 1) << 7) | (r << 2) -- byte k of every dword in a plane of its own
+// (two planes share a 256-byte column), so a lane's 16 contiguous bytes (one
+// load) map to rows r = o / 4 of their dwords, and the banks stay distinct by
+// rotating each group's dword order (below).
+__device__ __forceinline__ uint32_t tw_addr(uint32_t q, uint32_t b)
+{
+    return (((q & 3) >> 1) << 16) | (b << 8) | ((q & 1) << 7) | ((q >> 2) << 2);
+}
+#else
 __device__ __forceinline__ uint32_t tw_addr(uint32_t q, uint32_t b)
 {
     return ((q >> 6) << 16) | (b << 8) | ((q & 63) << 2);
 }
+#endif
 
+#if RAMCRC_TINY_LD16
+__device__ __forceinline__ void tiny_fill_wr(uint8_t* lds)
+{
+    // plane kk, column b, row r (r = q >> 2): X^(128 - q)(b), q = 4 r + kk, from
+    // g_tab.post word 128 (255 - b) + q; one 16-byte LDS chunk = rows 4 c .. 4 c + 3
+    // at tw_addr(16 c + kk, b)
+    constexpr uint32_t kChunks = 4 * 256 * 8, kAll = kChunks + 256;
+    constexpr uint32_t kPer = (kAll + kEntWaves * kWaveSize - 1) / (kEntWaves * kWaveSize);
+    const uint32_t* post = g_tab.post;
+    const uint4* inv = reinterpret_cast<const uint4*>(&g_tab.xinv128);
+    uint4 v[kPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+        const uint32_t i = threadIdx.x + j * (kEntWaves * kWaveSize);
+        if (i < kChunks) {
+            const uint32_t kk = i >> 11, b = (i >> 3) & 255, c = i & 7;
+            const uint32_t* w = post + 128 * (255 - b) + 16 * c + kk;
+            v[j] = make_uint4(w[0], w[4], w[8], w[12]);
+        } else if (i < kAll) {
+            v[j] = inv[i - kChunks];
+        }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+        const uint32_t i = threadIdx.x + j * (kEntWaves * kWaveSize);
+        if (i < kChunks) {
+            const uint32_t kk = i >> 11, b = (i >> 3) & 255, c = i & 7;
+            *reinterpret_cast<uint4*>(lds + tw_addr(16 * c + kk, b)) = v[j];
+        } else if (i < kAll) {
+            *reinterpret_cast<uint4*>(lds + kTwInvOff + 16 * (i - kChunks)) = v[j];
+        }
+    }
+}
+#else
 __device__ __forceinline__ void tiny_fill_wr(uint8_t* lds)
 {
     // 8192 chunks of 16 B, chunk (h, b, c) = words 128 (255 - b) + 64 h + 4 c .. of
@@ -1778,9 +1827,28 @@ __device__ __forceinline__ void tiny_fill_wr(uint8_t* lds)
             *reinterpret_cast<uint4*>(lds + 16 * i) = v[j];
     }
 }
+#endif
 
 // Per-lane address constants: byte k of a rotated dword (window position
 // 32 j + 4 u + ((k + g4) & 3)) of dword pair j >> 1; + 128 for odd j.
+#if RAMCRC_TINY_LD16
+// Lane u holds window bytes 16 u .. 16 u + 15 (one 16-byte load); at
+// instruction j it takes its dword (j + g4) & 3 -- window offset o = 16 u +
+// 4 ((j + g4) & 3) -- so the 32 lanes of a half-wave read 32 distinct rows
+// (banks).  P[j] = {o, o | 128, 1, 0}: one v_perm forms the address of byte
+// k of the dword (tw_addr(o + k, data byte)) from P[j] and the data.
+struct TwRows {
+    uint32_t P[4];
+    __device__ TwRows(uint32_t gl, uint32_t g4)
+    {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t o = 16 * gl + 4 * ((uint32_t(j) + g4) & 3);
+            P[j] = 0x00010000u | ((o | 128u) << 8) | o;
+        }
+    }
+};
+#else
 struct TwRows {
     uint32_t lr[2][4];
     __device__ TwRows(uint32_t gl, uint32_t g4)
@@ -1792,9 +1860,45 @@ struct TwRows {
                 lr[h][k] = (uint32_t(h) << 16) | (16 * gl + 4 * ((uint32_t(k) + g4) & 3));
     }
 };
+#endif
 
 // The group's sum over one window's bytes in [sa, e), byte b at position o
 // as X^(128 - o)(b) (relative to the window's end; all 8 lanes get it).
+#if RAMCRC_TINY_LD16
+__device__ __forceinline__ uint32_t tiny_win_wr(const uint8_t* lds, const u32x4& wv, uint32_t sa,
+                                                uint32_t e, const TwRows& rw, uint32_t gl, uint32_t g4)
+{
+    // this group's dword order: instruction j takes dword (j + g4) & 3
+    const uint32_t w0 = wv.x, w1 = wv.y, w2 = wv.z, w3 = wv.w;
+    const bool b0 = g4 & 1, b1 = g4 & 2;
+    const uint32_t t0 = b0 ? w1 : w0, t1 = b0 ? w2 : w1, t2 = b0 ? w3 : w2, t3 = b0 ? w0 : w3;
+    const uint32_t ws[4] = {b1 ? t2 : t0, b1 ? t3 : t1, b1 ? t0 : t2, b1 ? t1 : t3};
+    uint32_t v[16];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int o = int(rw.P[j] & 0xFF);   // the dword's window offset
+        // bytes of [sa, e): clamp(e - o, 0, 4) from the bottom, none below sa
+        const uint32_t sh = uint32_t(min(max(32 - 8 * (int(e) - o), 0), 32));
+        const uint32_t hd = uint32_t(min(max(8 * (int(sa) - o), 0), 32));
+        const uint32_t keep = uint32_t(uint64_t(0xFFFFFFFFu) >> sh) & uint32_t(~uint64_t(0) << hd);
+        const uint32_t x = ws[j] & keep;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            v[4 * j + k] = *reinterpret_cast<const uint32_t*>(
+                lds + __builtin_amdgcn_perm(x, rw.P[j],
+                                            0x0C000000u | ((k >> 1) ? 0x00020000u : 0x000C0000u) |
+                                                ((4u + uint32_t(k)) << 8) | uint32_t(k & 1)));
+    }
+    const uint32_t a0 = xor3(v[0], v[1], v[2]), a1 = xor3(v[3], v[4], v[5]);
+    const uint32_t a2 = xor3(v[6], v[7], v[8]), a3 = xor3(v[9], v[10], v[11]);
+    const uint32_t a4 = xor3(v[12], v[13], v[14]);
+    uint32_t R = xor3(xor3(a0, a1, a2), xor3(a3, a4, v[15]), 0u);
+    R ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(R), 0xB1, 0xF, 0xF, false));   // lane ^ 1
+    R ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(R), 0x4E, 0xF, 0xF, false));   // lane ^ 2
+    R ^= uint32_t(__builtin_amdgcn_ds_swizzle(int(R), 0x1F | (4 << 10)));           // lane ^ 4
+    return R;
+}
+#else
 __device__ __forceinline__ uint32_t tiny_win_wr(const uint8_t* lds, const u32x4& wv, uint32_t sa,
                                                 uint32_t e, const TwRows& rw, uint32_t gl, uint32_t g4)
 {
@@ -1827,6 +1931,7 @@ __device__ __forceinline__ uint32_t tiny_win_wr(const uint8_t* lds, const u32x4&
     R ^= uint32_t(__builtin_amdgcn_ds_swizzle(int(R), 0x1F | (4 << 10)));           // lane ^ 4
     return R;
 }
+#endif
 
 // X^m(v) for 4 <= m <= 128 (byte k at distance m - k), and X^-128(v)
 __device__ __forceinline__ uint32_t tw_shift(const uint8_t* lds, uint32_t v, uint32_t m)
@@ -1929,12 +2034,12 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
                                 swz_from<q>(uint32_t(o.S));
             // nothing to hash: the window loads read valid memory (the bin table)
             const uint64_t A = (geo[q] & 0xFFF) ? (Sq & ~uint64_t(15)) : dummy;
-            const uint64_t au = A + 4 * gl;
+            [[maybe_unused]] const uint64_t au = A + 4 * gl;
             u32x4 v;
             if (RAMCRC_TINY_SAFE && __builtin_amdgcn_ballot_w64(!((geo[q] >> 12) & 1)) == 0) {
                 // every window of this q is page-safe: plain loads, immediate offsets
-#if RAMCRC_TINY_LD4
-                v = load16(A + 16 * gl);   // A/B probe only (wrong CRCs): one 16-byte load per lane
+#if RAMCRC_TINY_LD4 || RAMCRC_TINY_LD16
+                v = load16(A + 16 * gl);   // (LD4: an A/B probe with the old layout, wrong CRCs)
 #else
                 v.x = *reinterpret_cast<g32*>(au);
                 v.y = *reinterpret_cast<g32*>(au + 32);
@@ -1943,11 +2048,17 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
 #endif
             } else {
                 const uint32_t e = ((geo[q] >> 8) & 0xF) + (geo[q] & 0xFF);   // E - A (0: empty)
+#if RAMCRC_TINY_LD16
+                // a piece at or past the entry's last byte reads that byte's piece
+                const uint32_t pl = (max(int(e) - 1, 0) & ~15);
+                v = load16(A + (16 * gl < pl ? 16 * gl : pl));
+#else
                 const int el = (max(int(e) - 1, 0) & ~3) - int(4 * gl);   // last dword, from 4 u
                 v.x = *reinterpret_cast<g32*>(au + min(0, el));
                 v.y = *reinterpret_cast<g32*>(au + min(32, el));
                 v.z = *reinterpret_cast<g32*>(au + min(64, el));
                 v.w = *reinterpret_cast<g32*>(au + min(96, el));
+#endif
             }
             w[q] = v;
         });
@@ -2142,6 +2253,17 @@ __device__ __forceinline__ void tiny_multi(const BatchDesc& d, const Sorted& so,
     auto load_entry = [&](uint32_t geo, uint64_t S, u32x4 (&w)[kTinyK]) {
         const uint32_t K = tk_windows(geo);
         const uint32_t el = (geo & 0x3FF) - tk_tail(geo) - 128 * (K - 1);   // last window's end
+#if RAMCRC_TINY_LD16
+        const uint64_t A = S & ~uint64_t(15);
+#pragma unroll
+        for (int k = 0; k < kTinyK; k++) {
+            if (uint32_t(k) < K) {
+                const uint32_t e = uint32_t(k) + 1 == K ? el : 128u;
+                const uint32_t pl = (max(int(e) - 1, 0) & ~15);
+                w[k] = load16(A + 128 * uint64_t(k) + (16 * gl < pl ? 16 * gl : pl));
+            }
+        }
+#else
         const uint64_t au = (S & ~uint64_t(15)) + 4 * gl;
 #pragma unroll
         for (int k = 0; k < kTinyK; k++) {
@@ -2155,6 +2277,7 @@ __device__ __forceinline__ void tiny_multi(const BatchDesc& d, const Sorted& so,
                 w[k].w = *reinterpret_cast<g32*>(aw + min(96, lim));
             }
         }
+#endif
     };
 
     uint64_t r = wave;
