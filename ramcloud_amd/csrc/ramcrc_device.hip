@@ -530,20 +530,26 @@ __device__ __forceinline__ uint32_t replay_header_bytes(uint32_t type)
     }
 }
 
+// The object bytes [S, E) of walk record r ({segment, offset, length,
+// header}); false (S == E) unless it is an object of a segment that passed.
+__device__ __forceinline__ bool record_range(const BatchDesc& d, const u32x4& r, uint64_t& S, uint64_t& E)
+{
+    const uint64_t payload = reinterpret_cast<uint64_t>(d.base) + uint64_t(r.x) * d.seg_bytes + r.y + 1 +
+                             ((r.w >> 6) & 3) + 1;
+    const bool obj = (r.w & (0x3f | kRecOverlong)) == RAMCRC_LOG_ENTRY_TYPE_OBJ && r.z >= kObjHeaderBytes &&
+                     (d.seg_status[r.x].x & RAMCRC_SEG_OK);
+    S = payload + 4;
+    E = obj ? payload + r.z : S;
+    return obj;
+}
+
 // [S, E) of buffer i; false for an inactive record (then S == E).
 template <int kMode>
 __device__ __forceinline__ bool buffer_range(const BatchDesc& d, uint64_t i, uint64_t& S,
                                              uint64_t& E)
 {
     if (kMode == kRecords) {
-        const u32x4 r = d.rec[i];   // {segment, offset, length, header}
-        const uint64_t payload = reinterpret_cast<uint64_t>(d.base) + uint64_t(r.x) * d.seg_bytes +
-                                 r.y + 1 + ((r.w >> 6) & 3) + 1;
-        const bool obj = (r.w & (0x3f | kRecOverlong)) == RAMCRC_LOG_ENTRY_TYPE_OBJ &&
-                         r.z >= kObjHeaderBytes && (d.seg_status[r.x].x & RAMCRC_SEG_OK);
-        S = payload + 4;
-        E = obj ? payload + r.z : S;
-        return obj;
+        return record_range(d, d.rec[i], S, E);
     } else if (kMode == kObjects) {
         const uint64_t o = reinterpret_cast<uint64_t>(d.base) + d.off[i];
         const uint64_t L = d.len[i];
@@ -1144,12 +1150,24 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
     const uint64_t n = entry_count<kMode>(d);
     for (uint64_t base = uint64_t(blockIdx.x) * tile; base < n; base += uint64_t(gridDim.x) * tile) {
         uint64_t S[kBinPer], E[kBinPer];
-        bool act[kBinPer];
+        bool act[kBinPer], oth[kBinPer];
 #pragma unroll
         for (int q = 0; q < kBinPer; q++) {   // all loads first
             const uint64_t i = base + uint64_t(q) * blockDim.x + threadIdx.x;
             S[q] = E[q] = 0;
-            act[q] = i < n && buffer_range<kMode>(d, i, S[q], E[q]);
+            oth[q] = false;
+            if constexpr (kMode == kRecords) {
+                // (the record read once: its range and whether k_obj_compare needs it)
+                if (i < n) {
+                    const u32x4 r = d.rec[i];
+                    act[q] = record_range(d, r, S[q], E[q]);
+                    oth[q] = replay_other(r);
+                } else {
+                    act[q] = false;
+                }
+            } else {
+                act[q] = i < n && buffer_range<kMode>(d, i, S[q], E[q]);
+            }
         }
         uint32_t big = 0, inact = 0, other = 0;
 #pragma unroll
@@ -1157,10 +1175,7 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
             const bool large = skip_large && is_large(E[q] - S[q]);
             big += act[q] && large;
             inact += !act[q] && base + uint64_t(q) * blockDim.x + threadIdx.x < n;
-            if constexpr (kMode == kRecords) {
-                const uint64_t i = base + uint64_t(q) * blockDim.x + threadIdx.x;
-                other += i < n && replay_other(d.rec[i]);
-            }
+            other += oth[q];
             const bool active = act[q] && !large;
             const int b = active ? bin_of(S[q], E[q]) : 0;
             uint32_t unused;
