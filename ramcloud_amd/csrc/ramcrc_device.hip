@@ -4948,7 +4948,10 @@ __global__ __launch_bounds__(256) void k_walk_emit(PWalk w0)
 // the segment's base), so a wave takes kCopyU blocks at a time and issues
 // each level's loads for all of them together.
 static_assert(kPartRec == kWaveSize, "k_walk_copy: one lane per record of a block");
-constexpr int kCopyU = 4;
+#ifndef RAMCRC_COPY_U
+#define RAMCRC_COPY_U 4
+#endif
+constexpr int kCopyU = RAMCRC_COPY_U;
 __global__ __launch_bounds__(256) void k_walk_copy(PWalk w0)
 {
     const PWalk w = walk_geo(w0);
