@@ -924,6 +924,9 @@ constexpr int kPU = RAMCRC_PU;             // ping-pong depth (pipelined bins)
 #ifndef RAMCRC_TINY_SAFE
 #define RAMCRC_TINY_SAFE 1    // tiny_run_cf: unclamped window loads when every window of a q is page-safe
 #endif
+#ifndef RAMCRC_TINY_EARLY
+#define RAMCRC_TINY_EARLY 0   // tiny phase: round 0's window loads issued before the table fill
+#endif
 #ifndef RAMCRC_TINY_LD16
 #define RAMCRC_TINY_LD16 0   // tiny phases: one 16-byte load per lane per window (layout above)
 #endif
@@ -2087,6 +2090,13 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
 
     uint64_t r = wave;
     TinyOwn o0 = load_own(r), o1 = load_own(r + nwaves);
+    u32x4 wc[8];
+    uint32_t gc[8], sc;
+#if RAMCRC_TINY_EARLY
+    // round 0's windows in flight while the table is filled (the fill's own
+    // loads are issued after them, so their waits cover both: max, not sum)
+    issue(o0, wc, gc, sc);
+#endif
 #if RAMCRC_TINY_WR
     tiny_fill_wr(lds);
     const TwRows rw(gl, g4);
@@ -2097,9 +2107,9 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
         return false;
     RAMCRC_STAMP(5);
     bool first_round = true;
-    u32x4 wc[8];
-    uint32_t gc[8], sc;
+#if !RAMCRC_TINY_EARLY
     issue(o0, wc, gc, sc);
+#endif
     for (; r < rounds; r += nwaves) {
         const TinyOwn o2 = load_own(r + 2 * nwaves);
         u32x4 wn[8];
