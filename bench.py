@@ -788,7 +788,10 @@ def run_replay(args, ranks):
                      "achieved": round(achieved, 1) if achieved else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                     "traffic": None, "scan_ms_per_step": round(scan_s * 1e3, 4)},
+                     "traffic": traffic_for(f"replay_{nseg}x{args.seg_mib}MiB_v{args.value_len}_k_entries")[0],
+                     "traffic_source": traffic_for(
+                         f"replay_{nseg}x{args.seg_mib}MiB_v{args.value_len}_k_entries")[1],
+                     "scan_ms_per_step": round(scan_s * 1e3, 4)},
         "cpu_baseline": cpu,
         "all_segments_verified": ok,
     }

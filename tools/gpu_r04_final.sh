@@ -22,3 +22,5 @@ timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o c3 -- pytho
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o c3_100 -- python bench.py --config entries --entry-size 100 --steps 10 --no-cpu-baseline > "$OUT/prof_c3_100.json" 2> "$OUT/prof_c3_100.err" || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o replay -- python bench.py --config replay --steps 10 --no-cpu-baseline > "$OUT/prof_replay.json" 2> "$OUT/prof_replay.err" || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o replay64 -- python bench.py --config replay --value-len 64 --steps 10 --no-cpu-baseline > "$OUT/prof_replay64.json" 2> "$OUT/prof_replay64.err" || exit 1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_replay" -o p -- python3 bench.py --config replay --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/pmc_replay.json" 2> "$OUT/pmc_replay.err" || exit 1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_replay64" -o p -- python3 bench.py --config replay --value-len 64 --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/pmc_replay64.json" 2> "$OUT/pmc_replay64.err" || exit 1
