@@ -906,7 +906,7 @@ constexpr int kSmallK = RAMCRC_SMALLK;     // bins 2..kSmallK: octets loaded one
 // bins 2 .. kTinyK (entries of 2 .. kTinyK windows, e.g. objects of 129 ..
 // ~500 B): the multi-window tiny phase (tiny_run_cf<true>); 1 = off (the short bins)
 constexpr int kTinyK = RAMCRC_TINY_K;
-static_assert(kTinyK >= 1 && kTinyK <= 4, "tiny windows: e_tot fits 10 bits");
+static_assert(kTinyK >= 1 && kTinyK <= 7, "tiny windows: E - A (<= 128 kTinyK) fits 10 bits");
 static_assert(kTinyK == 1 || RAMCRC_TINY_WR, "tiny_multi uses the window-relative table");
 #ifndef RAMCRC_ENT_NT
 #define RAMCRC_ENT_NT 1
