@@ -962,6 +962,13 @@ static_assert(RAMCRC_ENT_WAVES % 4 == 0, "age ranks of four waves");
 #define RAMCRC_BIN_PER 4
 #endif
 constexpr int kBinPer = RAMCRC_BIN_PER;    // entries per thread per tile (count/scatter)
+#ifndef RAMCRC_BIN_ONE
+#define RAMCRC_BIN_ONE 1   // k_bin_one for batches of <= 1 tile per workgroup (A/B: 0)
+#endif
+#ifndef RAMCRC_BIN_SLICES
+#define RAMCRC_BIN_SLICES 8   // k_bin_one: histogram copies (workgroup i adds to copy i % 8: its XCD's)
+#endif
+constexpr int kBinSlices = RAMCRC_BIN_SLICES;
 #ifndef RAMCRC_BIN_WGS_PER_CU
 #define RAMCRC_BIN_WGS_PER_CU 8
 #endif
@@ -1022,7 +1029,11 @@ struct BinCounters {
     uint32_t nlarge;          // large buffers the count pass left to k_chunks (skip_large)
     uint32_t ninact;          // inactive records (records mode: not checked here)
     uint32_t nother;          // records mode: records k_obj_compare has work for (replay_other)
+    uint32_t arrive;          // k_bin_one: workgroups past their histogram atomics
+    uint32_t flag;            // k_bin_one: raised by the last arrival
     uint32_t pad_;
+    uint32_t hs[kBinSlices][kNB];   // k_bin_one: histogram per slice of workgroups
+    uint32_t arr[kBinSlices];       // k_bin_one: arrivals per slice
 };
 
 struct BinTable {
@@ -1043,6 +1054,7 @@ struct Sorted {
     uint32_t* status;  // context status word (bit 2: inconsistent bin layout)
     uint64_t cap;      // sorted slots allocated
     uint32_t par;      // counter copy of this sequence
+    uint32_t one;      // host: the sequence was binned by k_bin_one (no scatter launch)
 };
 
 // First window of an entry in k_entries: its 128-byte line, so that every
@@ -1135,10 +1147,16 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
             nx.cursor[t] = 0;
             nx.hist[t] = 0;
         }
+        for (int t = threadIdx.x; t < kBinSlices * kNB; t += blockDim.x)
+            nx.hs[t / kNB][t % kNB] = 0;
+        for (int t = threadIdx.x; t < kBinSlices; t += blockDim.x)
+            nx.arr[t] = 0;
         if (threadIdx.x == 0) {
             nx.nlarge = 0;
             nx.ninact = 0;
             nx.nother = 0;
+            nx.arrive = 0;
+            nx.flag = 0;
         }
     }
     for (int t = threadIdx.x; t < kNB; t += blockDim.x)
@@ -1229,14 +1247,23 @@ struct BinScratch {
 // hold all of them), the layout is published empty with direct_n set and
 // nothing is scattered: k_entries' tiny phase reads the caller's (off, len,
 // init) in place, in index order.
+// A counter another workgroup of the same launch may have added to
+// (k_bin_one): read at the coherence point, not from this XCD's L2.
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ bool bin_layout(const Sorted& so, BinScratch& sc, bool publish,
-                                          uint64_t direct_n)
+                                          uint64_t direct_n, const uint32_t* hist = nullptr)
 {
     BinTable* bt = so.bt;
     const BinCounters& ctr = bt->ctr[so.par];
     const int b = threadIdx.x, lane = b & 63, w = b >> 6;
     if (threadIdx.x == 0)
-        sc.direct = direct_n && uint64_t(ctr.hist[0]) + ctr.hist[1] + ctr.ninact == direct_n;
+        sc.direct = direct_n && uint64_t(hist ? hist[0] : ld_agent(&ctr.hist[0])) +
+                                        (hist ? hist[1] : ld_agent(&ctr.hist[1])) +
+                                        ld_agent(&ctr.ninact) == direct_n;
     __syncthreads();
     const bool direct = sc.direct;
     if (publish && threadIdx.x == 0)
@@ -1244,7 +1271,7 @@ __device__ __forceinline__ bool bin_layout(const Sorted& so, BinScratch& sc, boo
     uint64_t cnt = 0, kc = 0, ps = 0, is = 0, pos_c = 0, item_c = 0;
     if (b < 256) {
         if (b < kNB) {
-            cnt = direct ? 0 : ctr.hist[b];
+            cnt = direct ? 0 : (hist ? hist[b] : ld_agent(&ctr.hist[b]));
             kc = b <= 32 ? uint64_t(b == 0 ? 1 : b) : bin_kmax(b);
         }
         const uint64_t oct = (cnt + kG - 1) / kG;
@@ -1366,6 +1393,194 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter(BatchDesc d, Sorted so
             }
         }
         __syncthreads();
+    }
+}
+
+// One-launch binning for batches of at most one tile per workgroup, with the
+// whole grid resident (bin_begin checks both): each workgroup loads its tile
+// once, ranks every entry inside its bin with the same wave_bin_add as the
+// count pass, and takes its range of each bin with one returning atomic on
+// the histogram -- the value the two-launch path's scatter cursor would give.
+// After a grid-wide arrival count (vector atomics; bounded spin, so a grid
+// that is not resident after all gives up, sets the status bits and
+// k_entries refuses instead of hanging) every workgroup lays the bins out
+// from the now complete histogram and writes its descriptors from registers.
+// Saves the scatter's launch and its second read of the table.
+#ifndef RAMCRC_BIN_SLEEP
+#define RAMCRC_BIN_SLEEP 4   // s_sleep between polls (x 64 cycles)
+#endif
+// No fences: on this 8-XCD part an agent-scope release / acquire writes back
+// / invalidates the XCD's L2 (per thread), which cost more than the whole
+// two-launch binning.  Everything that crosses workgroups here is an atomic
+// (the histogram adds, performed before the wave passes s_waitcnt, the
+// arrival count, the flag, and bin_layout's reads of the histogram).
+// Two-level arrival: a workgroup counts itself in its slice (workgroups
+// i % kBinSlices), the last of a slice counts the slice in `arrive`, the last
+// slice raises the flag (one counter for the whole grid serialised its
+// ~1,000 arrivals: ~5 us).  Returns false if the flag never came.
+__device__ __forceinline__ bool grid_arrive(BinCounters& ctr, uint32_t nwg)
+{
+    __shared__ uint32_t all_in;
+    __builtin_amdgcn_s_waitcnt(0);   // this wave's histogram atomics are performed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t sl = blockIdx.x % kBinSlices;
+        const uint32_t in_sl = nwg / kBinSlices + (sl < nwg % kBinSlices ? 1u : 0u);
+        const uint32_t nsl = nwg < uint32_t(kBinSlices) ? nwg : uint32_t(kBinSlices);
+        bool last = __hip_atomic_fetch_add(&ctr.arr[sl], 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT) + 1 == in_sl;
+        if (last)
+            last = __hip_atomic_fetch_add(&ctr.arrive, 1u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT) + 1 == nsl;
+        bool in = true;
+        if (last) {
+            __hip_atomic_store(&ctr.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            const uint32_t limit = (1u << 30) / (64u * RAMCRC_BIN_SLEEP + 64u);   // > 0.5 s
+            uint32_t spins = 0;
+            while (__hip_atomic_load(&ctr.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+                if (++spins > limit) {   // not resident after all: give up
+                    in = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(RAMCRC_BIN_SLEEP);
+            }
+        }
+        all_in = in;
+    }
+    __syncthreads();
+    return all_in;
+}
+
+template <int kMode>
+__global__ __launch_bounds__(kThreads) void k_bin_one(BatchDesc d, Sorted so, int skip_large)
+{
+    __shared__ uint32_t h[kNB];
+    __shared__ uint64_t base[kNB];
+    __shared__ uint32_t nlarge, ninact, nother;
+    __shared__ BinScratch sc;
+    BinCounters& ctr = so.bt->ctr[so.par];
+    if (blockIdx.x == 0) {
+        BinCounters& nx = so.bt->ctr[so.par ^ 1];   // the next sequence's counters
+        for (int t = threadIdx.x; t < kNB; t += blockDim.x) {
+            nx.cursor[t] = 0;
+            nx.hist[t] = 0;
+        }
+        for (int t = threadIdx.x; t < kBinSlices * kNB; t += blockDim.x)
+            nx.hs[t / kNB][t % kNB] = 0;
+        for (int t = threadIdx.x; t < kBinSlices; t += blockDim.x)
+            nx.arr[t] = 0;
+        if (threadIdx.x == 0) {
+            nx.nlarge = 0;
+            nx.ninact = 0;
+            nx.nother = 0;
+            nx.arrive = 0;
+            nx.flag = 0;
+        }
+    }
+    for (int t = threadIdx.x; t < kNB; t += blockDim.x)
+        h[t] = 0;
+    if (threadIdx.x == 0) {
+        nlarge = 0;
+        ninact = 0;
+        nother = 0;
+    }
+    __syncthreads();
+    const uint64_t n = entry_count<kMode>(d);
+    const uint64_t t0 = uint64_t(blockIdx.x) * blockDim.x * kBinPer;
+    uint64_t S[kBinPer], E[kBinPer];
+    bool act[kBinPer], oth[kBinPer];
+    uint32_t in0[kBinPer];
+#pragma unroll
+    for (int q = 0; q < kBinPer; q++) {   // all loads first
+        const uint64_t i = t0 + uint64_t(q) * blockDim.x + threadIdx.x;
+        S[q] = E[q] = 0;
+        oth[q] = false;
+        if constexpr (kMode == kRecords) {
+            if (i < n) {
+                const u32x4 r = d.rec[i];
+                act[q] = record_range(d, r, S[q], E[q]);
+                oth[q] = replay_other(r);
+            } else {
+                act[q] = false;
+            }
+        } else {
+            act[q] = i < n && buffer_range<kMode>(d, i, S[q], E[q]);
+        }
+        in0[q] = d.init && i < n ? d.init[i] : 0u;
+    }
+    int b[kBinPer];
+    uint32_t lp[kBinPer];
+    uint32_t big = 0, inact = 0, other = 0;
+#pragma unroll
+    for (int q = 0; q < kBinPer; q++) {
+        const bool large = skip_large && is_large(E[q] - S[q]);
+        big += act[q] && large;
+        inact += !act[q] && t0 + uint64_t(q) * blockDim.x + threadIdx.x < n;
+        other += oth[q];
+        const bool active = act[q] && !large;
+        b[q] = active ? bin_of(S[q], E[q]) : 0;
+        uint32_t wbase;
+        const uint32_t rank = wave_bin_add(h, b[q], active, wbase);
+        lp[q] = wbase + rank;
+        if (!active)
+            b[q] = -1;
+    }
+    if (__ballot(big != 0) && big)
+        atomicAdd(&nlarge, big);
+    if (kMode == kRecords && __ballot(inact != 0) && inact)
+        atomicAdd(&ninact, inact);
+    if (kMode == kRecords && __ballot(other != 0) && other)
+        atomicAdd(&nother, other);
+    __syncthreads();
+    const int sl = int(blockIdx.x % kBinSlices);
+    for (int t = threadIdx.x; t < kNB; t += blockDim.x)
+        base[t] = h[t] ? atomicAdd(&ctr.hs[sl][t], h[t]) : 0u;
+    if (threadIdx.x == 0 && nlarge)
+        atomicAdd(&ctr.nlarge, nlarge);
+    if (threadIdx.x == 0 && ninact)
+        atomicAdd(&ctr.ninact, ninact);
+    if (threadIdx.x == 0 && nother)
+        atomicAdd(&ctr.nother, nother);
+    if (!grid_arrive(ctr, gridDim.x)) {
+        if (threadIdx.x == 0)
+            atomicOr(so.status, kStatusSticky | kStatusBins);
+        return;
+    }
+    // totals, and this workgroup's place behind the earlier slices (reading
+    // the slices here beat having the last arrival publish the totals)
+    for (int t = threadIdx.x; t < kNB; t += blockDim.x) {
+        uint32_t all = 0, before = 0;
+#pragma unroll
+        for (int j = 0; j < kBinSlices; j++) {
+            const uint32_t v = ld_agent(&ctr.hs[j][t]);
+            before += j < sl ? v : 0u;
+            all += v;
+        }
+        h[t] = all;
+        base[t] += before;
+        if (blockIdx.x == 0)
+            ctr.hist[t] = all;
+    }
+    __syncthreads();
+    const bool ok = bin_layout(so, sc, blockIdx.x == 0,
+                               (kMode == kTable || kMode == kRecords) && RAMCRC_TINY_CF ? n : 0, h);
+    if (blockIdx.x == 0)   // what k_entries checks: every bin holds what was placed in it
+        for (int t = threadIdx.x; t < kNB; t += blockDim.x)
+            ctr.cursor[t] = sc.count[t];
+    if (!ok || sc.direct)
+        return;
+#pragma unroll
+    for (int q = 0; q < kBinPer; q++) {
+        if (b[q] >= 0 && base[b[q]] + lp[q] < sc.count[b[q]]) {
+            const uint64_t i = t0 + uint64_t(q) * blockDim.x + threadIdx.x;
+            const uint64_t pos = sc.start[b[q]] + base[b[q]] + lp[q];
+            so.desc[pos] = u32x4{uint32_t(S[q]), uint32_t(S[q] >> 32), uint32_t(E[q]),
+                                 uint32_t(E[q] >> 32)};
+            so.idx[pos] = uint32_t(i);
+            if (d.init)
+                so.init[pos] = in0[q];
+        }
     }
 }
 
@@ -3215,8 +3430,10 @@ int reserve_sorted(ramcrc_ctx* c, uint64_t n)
 
 // Small-entry path: bin by step count, scatter into bin order, scan.  A
 // binning sequence is k_bin_count (bin_begin) ... k_bin_scatter, k_entries
-// (bin_finish); the planned path runs its chunk kernels in between, so that
-// they can exit at once when the count pass found no large buffer.
+// (bin_finish), or k_bin_one (bin_begin) ... k_entries for a batch of at most
+// one tile per resident workgroup; the planned path runs its chunk kernels in
+// between, so that they can exit at once when the count pass found no large
+// buffer.
 uint64_t bin_grid(const ramcrc_ctx* c, uint64_t n)
 {
     // One tile per workgroup up to kBinWgsPerCu workgroups per CU: the binning
@@ -3236,7 +3453,7 @@ int bin_begin(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_large, 
     int rc = reserve_sorted(c, d.n);
     if (rc)
         return rc;
-    *so = Sorted{c->bins, c->sdesc, c->sidx, c->sinit, c->status, c->sorted_cap, c->bin_par};
+    *so = Sorted{c->bins, c->sdesc, c->sidx, c->sinit, c->status, c->sorted_cap, c->bin_par, 0};
     // Every launch of this library checks its own error right after it (the
     // timed ScanTimer::launch calls included), so an error pending here was left
     // by a caller's own HIP call on this thread (torch's pointer probes leave
@@ -3244,8 +3461,28 @@ int bin_begin(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_large, 
     // not reported as this launch's failure.
     if (hipError_t stale = hipGetLastError(); stale != hipSuccess)
         t_last_hip = int(stale);
-    hipLaunchKernelGGL(k_bin_count<kMode>, dim3(bin_grid(c, d.n)), dim3(kThreads), 0, s, d, *so,
-                       skip_large);
+    // One launch when one tile per workgroup covers the batch and that grid
+    // is resident at once (k_bin_one's arrival count needs every workgroup):
+    // at most half the workgroups a CU holds, so that a second context's
+    // k_bin_one on another stream fits beside it.  The dirty-histogram test
+    // hook needs the two-launch path.
+    const uint64_t tiles = (d.n + uint64_t(kThreads) * kBinPer - 1) / (uint64_t(kThreads) * kBinPer);
+    static int resident = -1;   // k_bin_one workgroups per CU
+    if (resident < 0) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_bin_one<kMode>, kThreads, 0) !=
+            hipSuccess)
+            nb = 0;
+        resident = nb;
+    }
+    if (RAMCRC_BIN_ONE && !c->dirty_bins && tiles > 0 &&
+        tiles <= uint64_t(c->ncu) * uint64_t(std::min(resident / 2, int(kBinWgsPerCu)))) {
+        so->one = 1;
+        hipLaunchKernelGGL(k_bin_one<kMode>, dim3(tiles), dim3(kThreads), 0, s, d, *so, skip_large);
+    } else {
+        hipLaunchKernelGGL(k_bin_count<kMode>, dim3(bin_grid(c, d.n)), dim3(kThreads), 0, s, d,
+                           *so, skip_large);
+    }
     HIPCHK(hipGetLastError());
     // enqueued: it zeroes the other copy, which the next sequence uses
     c->bin_par ^= 1u;
@@ -3265,9 +3502,11 @@ int bin_finish(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_large,
         c->dirty_bins = 0;
         HIPCHK(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_bin_scatter<kMode>, dim3(bin_grid(c, d.n)), dim3(kThreads), 0, s, d, so,
-                       skip_large);
-    HIPCHK(hipGetLastError());
+    if (!so.one) {
+        hipLaunchKernelGGL(k_bin_scatter<kMode>, dim3(bin_grid(c, d.n)), dim3(kThreads), 0, s, d,
+                           so, skip_large);
+        HIPCHK(hipGetLastError());
+    }
     {
         ScanTimer t(c, s);
         t.launch(k_entries, dim3(c->ncu), dim3(kEntWaves * kWaveSize), d, so);

@@ -1,5 +1,6 @@
-"""The small-entry binning sequence (k_bin_count -> k_bin_scatter -> k_entries)
-across failed and corrupted launches.
+"""The small-entry binning sequence (k_bin_count -> k_bin_scatter -> k_entries,
+or k_bin_one -> k_entries for batches of at most one tile per resident
+workgroup) across failed and corrupted launches.
 
 Round 2 recorded a GPU hang in k_entries whose cause was a bin layout that
 disagreed with the slots the scatter had written (stale slots, an octet of
@@ -176,4 +177,28 @@ def test_all_tiny_batch_direct_path(ctx, ramcrc, oracle_mod, api):
     assert np.array_equal(got, oracle_mod.entries(host, offs, lens2))
     got = host_u32(run(ctx, api, base, offs, lens))
     assert np.array_equal(got, oracle_mod.entries(host, offs, lens))
+    ctx.check()
+
+
+@pytest.mark.parametrize("api", ["entries", "batch"])
+def test_one_launch_threshold(ctx, oracle_mod, api):
+    """Batches either side of the one-launch binning limit (one 1,024-entry
+    tile per workgroup, four workgroups per CU: 1,048,576 entries on 256 CUs)
+    and a few small ones: k_bin_one and the two-launch path give the same,
+    exact CRCs, with and without initial states."""
+    rng = np.random.default_rng(5150)
+    total = 4 << 20
+    host = oracle_mod.splitmix_bytes(31, total)
+    base = dev(host)
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    lim = ncu * 4 * 1024
+    for n in (1, 1023, 1025, lim - 1, lim, lim + 1):
+        lens = rng.integers(0, 600, n)
+        lens[::7] = rng.integers(600, 9000, lens[::7].size)
+        offs = rng.integers(0, total - 9000, n)
+        init = None if n % 2 else rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+        got = host_u32(run(ctx, api, base, offs, lens, init))
+        want = oracle_mod.entries(host, offs, lens, init=init)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (n, [(int(offs[i]) % 128, int(lens[i])) for i in bad[:8]])
     ctx.check()
