@@ -532,15 +532,22 @@ __device__ __forceinline__ uint32_t replay_header_bytes(uint32_t type)
 
 // The object bytes [S, E) of walk record r ({segment, offset, length,
 // header}); false (S == E) unless it is an object of a segment that passed.
-__device__ __forceinline__ bool record_range(const BatchDesc& d, const u32x4& r, uint64_t& S, uint64_t& E)
+// (seg_st: the flags word of the record's segment status)
+__device__ __forceinline__ bool record_range_st(const BatchDesc& d, const u32x4& r, uint32_t seg_st,
+                                                uint64_t& S, uint64_t& E)
 {
     const uint64_t payload = reinterpret_cast<uint64_t>(d.base) + uint64_t(r.x) * d.seg_bytes + r.y + 1 +
                              ((r.w >> 6) & 3) + 1;
     const bool obj = (r.w & (0x3f | kRecOverlong)) == RAMCRC_LOG_ENTRY_TYPE_OBJ && r.z >= kObjHeaderBytes &&
-                     (d.seg_status[r.x].x & RAMCRC_SEG_OK);
+                     (seg_st & RAMCRC_SEG_OK);
     S = payload + 4;
     E = obj ? payload + r.z : S;
     return obj;
+}
+
+__device__ __forceinline__ bool record_range(const BatchDesc& d, const u32x4& r, uint64_t& S, uint64_t& E)
+{
+    return record_range_st(d, r, d.seg_status[r.x].x, S, E);
 }
 
 // [S, E) of buffer i; false for an inactive record (then S == E).
@@ -969,6 +976,9 @@ constexpr int kBinPer = RAMCRC_BIN_PER;    // entries per thread per tile (count
 #define RAMCRC_BIN_SLICES 8   // k_bin_one: histogram copies (workgroup i adds to copy i % 8: its XCD's)
 #endif
 constexpr int kBinSlices = RAMCRC_BIN_SLICES;
+#ifndef RAMCRC_COUNT_PF
+#define RAMCRC_COUNT_PF 1   // k_bin_count, records: next tile's records in flight (A/B: 0)
+#endif
 #ifndef RAMCRC_BIN_WGS_PER_CU
 #define RAMCRC_BIN_WGS_PER_CU 8
 #endif
@@ -1169,9 +1179,47 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
     __syncthreads();
     const uint64_t tile = uint64_t(blockDim.x) * kBinPer;
     const uint64_t n = entry_count<kMode>(d);
+    // Records (replay batches of up to ~40M): the next tile's records are in
+    // flight while this tile's segment status words are read and binned.
+    // Order per tile: status loads (their records arrived last tile), then the
+    // next tile's record loads, then the wait for the status words only.
+    constexpr bool kPf = kMode == kRecords && RAMCRC_COUNT_PF;
+    [[maybe_unused]] u32x4 nr[kBinPer];
+    if constexpr (kPf) {
+#pragma unroll
+        for (int q = 0; q < kBinPer; q++) {
+            const uint64_t i = uint64_t(blockIdx.x) * tile + uint64_t(q) * blockDim.x + threadIdx.x;
+            nr[q] = i < n ? d.rec[i] : u32x4{0u, 0u, 0u, 0u};
+        }
+    }
     for (uint64_t base = uint64_t(blockIdx.x) * tile; base < n; base += uint64_t(gridDim.x) * tile) {
         uint64_t S[kBinPer], E[kBinPer];
         bool act[kBinPer], oth[kBinPer];
+        if constexpr (kPf) {
+            u32x4 cur[kBinPer];
+            uint32_t st[kBinPer];
+#pragma unroll
+            for (int q = 0; q < kBinPer; q++) {
+                cur[q] = nr[q];
+                const uint64_t i = base + uint64_t(q) * blockDim.x + threadIdx.x;
+                st[q] = i < n ? d.seg_status[cur[q].x].x : 0u;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            const uint64_t nb = base + uint64_t(gridDim.x) * tile;
+#pragma unroll
+            for (int q = 0; q < kBinPer; q++) {
+                const uint64_t i = nb + uint64_t(q) * blockDim.x + threadIdx.x;
+                nr[q] = i < n ? d.rec[i] : u32x4{0u, 0u, 0u, 0u};
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < kBinPer; q++) {
+                const uint64_t i = base + uint64_t(q) * blockDim.x + threadIdx.x;
+                S[q] = E[q] = 0;
+                act[q] = i < n && record_range_st(d, cur[q], st[q], S[q], E[q]);
+                oth[q] = i < n && replay_other(cur[q]);
+            }
+        } else {
 #pragma unroll
         for (int q = 0; q < kBinPer; q++) {   // all loads first
             const uint64_t i = base + uint64_t(q) * blockDim.x + threadIdx.x;
@@ -1189,6 +1237,7 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
             } else {
                 act[q] = i < n && buffer_range<kMode>(d, i, S[q], E[q]);
             }
+        }
         }
         uint32_t big = 0, inact = 0, other = 0;
 #pragma unroll
