@@ -453,6 +453,14 @@ int ramcrc_assemble_objects_host(ramcrc_ctx* ctx, void* const* objs, const uint6
  *                           the launch must then refuse (RAMCRC_EINTERNAL from
  *                           ramcrc_ctx_check) rather than read stale slots. */
 #define RAMCRC_OPT_TEST_DIRTY_BINS 4
+/*   RAMCRC_OPT_TEST_BIN_STRAGGLER  test hook: the next one-launch binning
+ *                           (k_bin_one, batches of at most one tile per
+ *                           resident workgroup) waits for one workgroup more
+ *                           than it launched, as if the grid were not resident;
+ *                           every workgroup gives up after 0.25 s and the
+ *                           launch must refuse (RAMCRC_EINTERNAL from
+ *                           ramcrc_ctx_check) instead of hanging. */
+#define RAMCRC_OPT_TEST_BIN_STRAGGLER 5
 int ramcrc_ctx_set_option(ramcrc_ctx* ctx, int option, int64_t value);
 
 /* Kernel timing (for benchmarks): when enabled, every launch brackets its

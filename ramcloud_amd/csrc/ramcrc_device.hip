@@ -1463,6 +1463,8 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter(BatchDesc d, Sorted so
 // two-launch binning.  Everything that crosses workgroups here is an atomic
 // (the histogram adds, performed before the wave passes s_waitcnt, the
 // arrival count, the flag, and bin_layout's reads of the histogram).
+constexpr uint64_t kBinSpinTicks = 25000000;   // k_bin_one gives up after 0.25 s
+
 // Two-level arrival: a workgroup counts itself in its slice (workgroups
 // i % kBinSlices), the last of a slice counts the slice in `arrive`, the last
 // slice raises the flag (one counter for the whole grid serialised its
@@ -1485,11 +1487,10 @@ __device__ __forceinline__ bool grid_arrive(BinCounters& ctr, uint32_t nwg)
         if (last) {
             __hip_atomic_store(&ctr.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            const uint32_t limit = (1u << 30) / (64u * RAMCRC_BIN_SLEEP + 64u);   // > 0.5 s
-            uint32_t spins = 0;
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
             while (__hip_atomic_load(&ctr.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-                if (++spins > limit) {   // not resident after all: give up
-                    in = false;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kBinSpinTicks) {
+                    in = false;   // not resident after all: give up
                     break;
                 }
                 __builtin_amdgcn_s_sleep(RAMCRC_BIN_SLEEP);
@@ -1502,7 +1503,8 @@ __device__ __forceinline__ bool grid_arrive(BinCounters& ctr, uint32_t nwg)
 }
 
 template <int kMode>
-__global__ __launch_bounds__(kThreads) void k_bin_one(BatchDesc d, Sorted so, int skip_large)
+__global__ __launch_bounds__(kThreads) void k_bin_one(BatchDesc d, Sorted so, int skip_large,
+                                                      uint32_t straggler)
 {
     __shared__ uint32_t h[kNB];
     __shared__ uint64_t base[kNB];
@@ -1591,9 +1593,14 @@ __global__ __launch_bounds__(kThreads) void k_bin_one(BatchDesc d, Sorted so, in
         atomicAdd(&ctr.ninact, ninact);
     if (threadIdx.x == 0 && nother)
         atomicAdd(&ctr.nother, nother);
-    if (!grid_arrive(ctr, gridDim.x)) {
-        if (threadIdx.x == 0)
+    // (straggler: test hook, one workgroup more than launched, which never comes)
+    if (!grid_arrive(ctr, gridDim.x + straggler)) {
+        // a layout k_entries cannot accept (count[0] = 2^64 - 1 matches no
+        // cursor), whatever the previous sequence published
+        if (threadIdx.x == 0) {
             atomicOr(so.status, kStatusSticky | kStatusBins);
+            so.bt->count[0] = ~0ull;
+        }
         return;
     }
     // totals, and this workgroup's place behind the earlier slices (reading
@@ -3292,6 +3299,7 @@ struct ramcrc_ctx {
     uint32_t bin_par = 0;   // counter copy of the next binning sequence (BinCounters)
     int fail_after_count = 0;   // RAMCRC_OPT_TEST_FAIL_AFTER_COUNT: abandon N sequences
     uint32_t dirty_bins = 0;    // RAMCRC_OPT_TEST_DIRTY_BINS: bin << 16 | count, once
+    int bin_straggler = 0;      // RAMCRC_OPT_TEST_BIN_STRAGGLER: next k_bin_one waits in vain
     u32x4* sdesc = nullptr;
     uint32_t* sidx = nullptr;
     uint32_t* sinit = nullptr;
@@ -3527,7 +3535,9 @@ int bin_begin(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_large, 
     if (RAMCRC_BIN_ONE && !c->dirty_bins && tiles > 0 &&
         tiles <= uint64_t(c->ncu) * uint64_t(std::min(resident / 2, int(kBinWgsPerCu)))) {
         so->one = 1;
-        hipLaunchKernelGGL(k_bin_one<kMode>, dim3(tiles), dim3(kThreads), 0, s, d, *so, skip_large);
+        hipLaunchKernelGGL(k_bin_one<kMode>, dim3(tiles), dim3(kThreads), 0, s, d, *so, skip_large,
+                           c->bin_straggler ? 1u : 0u);
+        c->bin_straggler = 0;
     } else {
         hipLaunchKernelGGL(k_bin_count<kMode>, dim3(bin_grid(c, d.n)), dim3(kThreads), 0, s, d,
                            *so, skip_large);
@@ -5665,6 +5675,9 @@ int ramcrc_ctx_set_option(ramcrc_ctx* c, int option, int64_t value)
         if (value < 0 || value > 0xFFFFFFFFll)
             return RAMCRC_EINVAL;
         c->dirty_bins = uint32_t(value);
+        return RAMCRC_OK;
+    case RAMCRC_OPT_TEST_BIN_STRAGGLER:
+        c->bin_straggler = value != 0;
         return RAMCRC_OK;
     case RAMCRC_OPT_WALK_PART_SHIFT:
         if (value != 0 && (value < kPartShiftMin || value > 20))

@@ -36,6 +36,7 @@ OPT_SERIAL_WALK = 1
 OPT_WALK_PART_SHIFT = 2
 OPT_TEST_FAIL_AFTER_COUNT = 3
 OPT_TEST_DIRTY_BINS = 4
+OPT_TEST_BIN_STRAGGLER = 5
 
 
 class RamcrcError(RuntimeError):

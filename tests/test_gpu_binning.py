@@ -202,3 +202,27 @@ def test_one_launch_threshold(ctx, oracle_mod, api):
         bad = np.nonzero(got != want)[0]
         assert bad.size == 0, (n, [(int(offs[i]) % 128, int(lens[i])) for i in bad[:8]])
     ctx.check()
+
+
+@pytest.mark.parametrize("api", ["entries", "batch"])
+def test_one_launch_binning_gives_up(ctx, ramcrc, oracle_mod, api):
+    """k_bin_one's grid-wide arrival waits for every workgroup it launched; if
+    one never comes (a grid that is not resident after all, forced here by the
+    straggler hook), every workgroup gives up after a bounded spin, the launch
+    is refused with RAMCRC_EINTERNAL instead of hanging, no small entry is
+    written, and the next call is exact."""
+    host, offs, ls, init = alignment_case(oracle_mod, seed=13)
+    base = dev(host)
+    sentinel = torch.full((len(offs),), 0x3C3C3C3C, dtype=torch.int32, device="cuda")
+    ctx.set_option(ramcrc.OPT_TEST_BIN_STRAGGLER, 1)
+    run(ctx, api, base, offs, ls, init, out=sentinel)
+    with pytest.raises(ramcrc.RamcrcError) as e:
+        ctx.check()
+    assert e.value.code == ramcrc.EINTERNAL
+    got = host_u32(sentinel)
+    small = np.array([L < 65536 for L in ls])
+    assert np.all(got[small] == 0x3C3C3C3C)
+    for it in (init, None):
+        got = host_u32(run(ctx, api, base, offs, ls, it))
+        assert np.array_equal(got, oracle_mod.entries(host, offs, ls, init=it))
+    ctx.check()
