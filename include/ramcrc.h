@@ -41,8 +41,12 @@ enum {
     RAMCRC_EREFUSED = -6, /* a launch found more chunks than the context's scratch holds and
                              wrote none of its outputs (see ramcrc_ctx_check) */
     RAMCRC_EINTERNAL = -7, /* a small-entry launch found its bin layout inconsistent with the
-                             entries it binned; its outputs are unspecified (an internal
-                             invariant; never expected -- see ramcrc_ctx_check) */
+                             entries it binned and wrote none of its small-entry outputs.
+                             Only a corrupted bin table produces it (the TEST_DIRTY_BINS
+                             hook does so on purpose); scheduling cannot: a one-launch
+                             binning whose grid is not all resident (other contexts'
+                             kernels, preemption) falls back to the two-launch binning
+                             inside the same call.  See ramcrc_ctx_check. */
     RAMCRC_EPEER = -8,    /* multi-GPU shard: this rank's part of the step succeeded but
                              another rank's failed; that rank's segments read 0xFFFFFFFF */
     RAMCRC_EORDER = -9    /* a RAMCRC_ORDERED batch was not in log order (entries overlap,
@@ -454,12 +458,12 @@ int ramcrc_assemble_objects_host(ramcrc_ctx* ctx, void* const* objs, const uint6
  *                           ramcrc_ctx_check) rather than read stale slots. */
 #define RAMCRC_OPT_TEST_DIRTY_BINS 4
 /*   RAMCRC_OPT_TEST_BIN_STRAGGLER  test hook: the next one-launch binning
- *                           (k_bin_one, batches of at most one tile per
- *                           resident workgroup) waits for one workgroup more
- *                           than it launched, as if the grid were not resident;
- *                           every workgroup gives up after 0.25 s and the
- *                           launch must refuse (RAMCRC_EINTERNAL from
- *                           ramcrc_ctx_check) instead of hanging. */
+ *                           (k_bin_one, batches of at most one 4,096-entry
+ *                           tile per CU) waits for one workgroup more than it
+ *                           launched, as if part of the grid were never
+ *                           dispatched; it must abort after its stall period
+ *                           (no arrival for 30 us) and the launch complete
+ *                           through the two-launch binning with exact results. */
 #define RAMCRC_OPT_TEST_BIN_STRAGGLER 5
 int ramcrc_ctx_set_option(ramcrc_ctx* ctx, int option, int64_t value);
 
@@ -506,7 +510,9 @@ int ramcrc_ctx_check(ramcrc_ctx* ctx, void* stream);
 
 /* Diagnostics.  ramcrc_ctx_debug_bins waits for the device and copies the
  * small-entry bin table's counts, both counter copies' cursors and
- * histograms (5 x 161 words) to host, and the parity of the next sequence. */
+ * histograms (5 x 161 words), then the number of one-launch binnings that
+ * aborted and completed through the two-launch path (1 word), to host, and
+ * the parity of the next sequence. */
 int ramcrc_ctx_debug_bins(ramcrc_ctx* ctx, uint64_t* host, uint64_t nwords, uint32_t* par_next);
 const char* ramcrc_strerror(int code);
 int ramcrc_last_hip_error(void);            /* last hipError_t seen (thread-local) */

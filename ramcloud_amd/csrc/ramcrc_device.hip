@@ -972,6 +972,10 @@ constexpr int kBinPer = RAMCRC_BIN_PER;    // entries per thread per tile (count
 #ifndef RAMCRC_BIN_ONE
 #define RAMCRC_BIN_ONE 1   // k_bin_one for batches of <= 1 tile per workgroup (A/B: 0)
 #endif
+#ifndef RAMCRC_BIN_RESCUE
+#define RAMCRC_BIN_RESCUE 1   // the guarded scatter after every k_bin_one (A/B only: 0 = none,
+                              // an aborted k_bin_one then leaves its batch unbinned)
+#endif
 #ifndef RAMCRC_BIN_SLICES
 #define RAMCRC_BIN_SLICES 8   // k_bin_one: histogram copies (workgroup i adds to copy i % 8: its XCD's)
 #endif
@@ -1040,11 +1044,13 @@ struct BinCounters {
     uint32_t ninact;          // inactive records (records mode: not checked here)
     uint32_t nother;          // records mode: records k_obj_compare has work for (replay_other)
     uint32_t arrive;          // k_bin_one: workgroups past their histogram atomics
-    uint32_t flag;            // k_bin_one: raised by the last arrival
+    uint32_t flag;            // k_bin_one: 0, then kBinGo (last arrival) or kBinAbort (a stall)
     uint32_t pad_;
     uint32_t hs[kBinSlices][kNB];   // k_bin_one: histogram per slice of workgroups
     uint32_t arr[kBinSlices];       // k_bin_one: arrivals per slice
 };
+
+constexpr uint32_t kBinGo = 1, kBinAbort = 2;   // BinCounters::flag: k_bin_one's vote
 
 struct BinTable {
     uint64_t start[kNB];      // first sorted slot of the bin (multiple of 8)
@@ -1054,6 +1060,7 @@ struct BinTable {
     uint64_t direct_n;        // nonzero: every entry of this kTable batch is tiny; the tiny
                               // phase reads the caller's table in place (nothing scattered)
     BinCounters ctr[2];       // per parity; copy p ^ 1 is zeroed by sequence p's k_bin_count
+    uint64_t rescues;         // k_bin_one launches that aborted and were binned by the guarded scatter
 };
 
 struct Sorted {
@@ -1382,20 +1389,43 @@ __device__ __forceinline__ bool bin_layout(const Sorted& so, BinScratch& sc, boo
     return true;
 }
 
+// rescue: the guarded scatter after a k_bin_one (see there): nothing to do
+// when k_bin_one's vote went kBinGo; otherwise the histogram is the sum of
+// k_bin_one's slices, which every workgroup of it added to before it voted.
 template <int kMode>
-__global__ __launch_bounds__(kThreads) void k_bin_scatter(BatchDesc d, Sorted so, int skip_large)
+__global__ __launch_bounds__(kThreads) void k_bin_scatter(BatchDesc d, Sorted so, int skip_large,
+                                                          int rescue)
 {
     __shared__ uint32_t cnt[kNB];
     __shared__ uint64_t base[kNB];
     __shared__ BinScratch sc;
+    __shared__ uint32_t tot[kNB];
+    BinCounters& ctr = so.bt->ctr[so.par];
+    if (rescue) {
+        if (ld_agent(&ctr.flag) == kBinGo)
+            return;   // (k_bin_one has ended: the flag is final and uniform)
+        for (int t = threadIdx.x; t < kNB; t += blockDim.x) {
+            uint32_t all = 0;
+#pragma unroll
+            for (int j = 0; j < kBinSlices; j++)
+                all += ld_agent(&ctr.hs[j][t]);
+            tot[t] = all;
+            if (blockIdx.x == 0)
+                ctr.hist[t] = all;
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            atomicAdd(reinterpret_cast<unsigned long long*>(&so.bt->rescues), 1ull);
+    }
     for (int t = threadIdx.x; t < kNB; t += blockDim.x)
         cnt[t] = 0;
+    __syncthreads();
     if (!bin_layout(so, sc, blockIdx.x == 0,
-                    (kMode == kTable || kMode == kRecords) && RAMCRC_TINY_CF ? entry_count<kMode>(d) : 0))
+                    (kMode == kTable || kMode == kRecords) && RAMCRC_TINY_CF ? entry_count<kMode>(d) : 0,
+                    rescue ? tot : nullptr))
         return;   // corrupted histogram: nothing is scattered, k_entries refuses
     if (sc.direct)
         return;   // all tiny: k_entries reads the table in place
-    unsigned long long* cursor = reinterpret_cast<unsigned long long*>(so.bt->ctr[so.par].cursor);
+    unsigned long long* cursor = reinterpret_cast<unsigned long long*>(ctr.cursor);
     const uint64_t tile = uint64_t(blockDim.x) * kBinPer;
     const uint64_t n = entry_count<kMode>(d);
     for (uint64_t t0 = uint64_t(blockIdx.x) * tile; t0 < n; t0 += uint64_t(gridDim.x) * tile) {
@@ -1446,29 +1476,62 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter(BatchDesc d, Sorted so
 }
 
 // One-launch binning for batches of at most one tile per workgroup, with the
-// whole grid resident (bin_begin checks both): each workgroup loads its tile
-// once, ranks every entry inside its bin with the same wave_bin_add as the
-// count pass, and takes its range of each bin with one returning atomic on
-// the histogram -- the value the two-launch path's scatter cursor would give.
-// After a grid-wide arrival count (vector atomics; bounded spin, so a grid
-// that is not resident after all gives up, sets the status bits and
-// k_entries refuses instead of hanging) every workgroup lays the bins out
+// grid expected resident at once (bin_begin checks both): each workgroup loads
+// its tile once, ranks every entry inside its bin with the same wave_bin_add
+// as the count pass, and takes its range of each bin with one returning
+// atomic on the histogram -- the value the two-launch path's scatter cursor
+// would give.  After a grid-wide arrival every workgroup lays the bins out
 // from the now complete histogram and writes its descriptors from registers.
-// Saves the scatter's launch and its second read of the table.
+// Saves the scatter's second read of the table.
+//
+// The arrival cannot be guaranteed: another context's kernels on another
+// stream (a k_entries workgroup takes a whole CU; a second k_bin_one takes
+// the other half) or a preempted queue can keep part of the grid from being
+// dispatched while the rest waits.  So the wait is a vote, never a
+// precondition: the last arrival tries to turn the flag from 0 to kBinGo, a
+// waiter that has seen no arrival anywhere in the grid for kBinStallTicks
+// tries to turn it from 0 to kBinAbort, and the one compare-and-swap that
+// wins decides for every workgroup, including those dispatched later.  On
+// abort nothing is scattered; the guarded scatter launched after every
+// k_bin_one (k_bin_scatter with `rescue`) exits at once on kBinGo and
+// otherwise bins the batch the two-launch way from the histogram k_bin_one
+// completed.  A grid that cannot all be resident therefore costs one stall
+// period and a second read of the table, never a wrong or refused launch.
 #ifndef RAMCRC_BIN_SLEEP
 #define RAMCRC_BIN_SLEEP 4   // s_sleep between polls (x 64 cycles)
+#endif
+#ifndef RAMCRC_BIN_STALL_US
+#define RAMCRC_BIN_STALL_US 30   // k_bin_one: abort after this long with no arrival in the grid
 #endif
 // No fences: on this 8-XCD part an agent-scope release / acquire writes back
 // / invalidates the XCD's L2 (per thread), which cost more than the whole
 // two-launch binning.  Everything that crosses workgroups here is an atomic
 // (the histogram adds, performed before the wave passes s_waitcnt, the
-// arrival count, the flag, and bin_layout's reads of the histogram).
-constexpr uint64_t kBinSpinTicks = 25000000;   // k_bin_one gives up after 0.25 s
+// arrival counts, the flag, and bin_layout's reads of the histogram).
+constexpr uint64_t kBinStallTicks = uint64_t(RAMCRC_BIN_STALL_US) * 100;   // 100 MHz clock
+__device__ __forceinline__ uint32_t bin_arrivals(const BinCounters& ctr)
+{
+    uint32_t a = 0;
+#pragma unroll
+    for (int j = 0; j < kBinSlices; j++)
+        a += __hip_atomic_load(&ctr.arr[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return a;
+}
+
+__device__ __forceinline__ uint32_t bin_vote(BinCounters& ctr, uint32_t want)
+{
+    uint32_t expect = 0;
+    __hip_atomic_compare_exchange_strong(&ctr.flag, &expect, want, __ATOMIC_RELAXED,
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return expect ? expect : want;   // the value that won
+}
 
 // Two-level arrival: a workgroup counts itself in its slice (workgroups
 // i % kBinSlices), the last of a slice counts the slice in `arrive`, the last
-// slice raises the flag (one counter for the whole grid serialised its
-// ~1,000 arrivals: ~5 us).  Returns false if the flag never came.
+// slice votes kBinGo (one counter for the whole grid serialised its ~1,000
+// arrivals: ~5 us).  Returns true when kBinGo won the vote.  The clock is the
+// 100 MHz s_memrealtime; a stall measured across a preemption only makes the
+// abort (the slower, always correct path) more likely.
 __device__ __forceinline__ bool grid_arrive(BinCounters& ctr, uint32_t nwg)
 {
     __shared__ uint32_t all_in;
@@ -1483,20 +1546,27 @@ __device__ __forceinline__ bool grid_arrive(BinCounters& ctr, uint32_t nwg)
         if (last)
             last = __hip_atomic_fetch_add(&ctr.arrive, 1u, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT) + 1 == nsl;
-        bool in = true;
+        uint32_t f;
         if (last) {
-            __hip_atomic_store(&ctr.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            f = bin_vote(ctr, kBinGo);
         } else {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz
-            while (__hip_atomic_load(&ctr.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-                if (__builtin_amdgcn_s_memrealtime() - t0 > kBinSpinTicks) {
-                    in = false;   // not resident after all: give up
-                    break;
+            uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            uint32_t seen = bin_arrivals(ctr);
+            while ((f = __hip_atomic_load(&ctr.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
+                const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                if (now - t0 > kBinStallTicks) {
+                    const uint32_t a = bin_arrivals(ctr);
+                    if (a == seen) {
+                        f = bin_vote(ctr, kBinAbort);   // nobody arrived for a whole period
+                        break;
+                    }
+                    seen = a;
+                    t0 = now;
                 }
                 __builtin_amdgcn_s_sleep(RAMCRC_BIN_SLEEP);
             }
         }
-        all_in = in;
+        all_in = f == kBinGo;
     }
     __syncthreads();
     return all_in;
@@ -1594,15 +1664,8 @@ __global__ __launch_bounds__(kThreads) void k_bin_one(BatchDesc d, Sorted so, in
     if (threadIdx.x == 0 && nother)
         atomicAdd(&ctr.nother, nother);
     // (straggler: test hook, one workgroup more than launched, which never comes)
-    if (!grid_arrive(ctr, gridDim.x + straggler)) {
-        // a layout k_entries cannot accept (count[0] = 2^64 - 1 matches no
-        // cursor), whatever the previous sequence published
-        if (threadIdx.x == 0) {
-            atomicOr(so.status, kStatusSticky | kStatusBins);
-            so.bt->count[0] = ~0ull;
-        }
-        return;
-    }
+    if (!grid_arrive(ctr, gridDim.x + straggler))
+        return;   // aborted: the guarded scatter bins the batch
     // totals, and this workgroup's place behind the earlier slices (reading
     // the slices here beat having the last arrival publish the totals)
     for (int t = threadIdx.x; t < kNB; t += blockDim.x) {
@@ -3300,6 +3363,7 @@ struct ramcrc_ctx {
     int fail_after_count = 0;   // RAMCRC_OPT_TEST_FAIL_AFTER_COUNT: abandon N sequences
     uint32_t dirty_bins = 0;    // RAMCRC_OPT_TEST_DIRTY_BINS: bin << 16 | count, once
     int bin_straggler = 0;      // RAMCRC_OPT_TEST_BIN_STRAGGLER: next k_bin_one waits in vain
+    int bin_resident[5] = {-1, -1, -1, -1, -1};   // k_bin_one<mode> workgroups per CU (occupancy query)
     u32x4* sdesc = nullptr;
     uint32_t* sidx = nullptr;
     uint32_t* sinit = nullptr;
@@ -3524,7 +3588,7 @@ int bin_begin(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_large, 
     // k_bin_one on another stream fits beside it.  The dirty-histogram test
     // hook needs the two-launch path.
     const uint64_t tiles = (d.n + uint64_t(kThreads) * kBinPer - 1) / (uint64_t(kThreads) * kBinPer);
-    static int resident = -1;   // k_bin_one workgroups per CU
+    int& resident = c->bin_resident[kMode];   // k_bin_one workgroups per CU (under c->mu)
     if (resident < 0) {
         int nb = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_bin_one<kMode>, kThreads, 0) !=
@@ -3561,9 +3625,10 @@ int bin_finish(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_large,
         c->dirty_bins = 0;
         HIPCHK(hipGetLastError());
     }
-    if (!so.one) {
+    if (!so.one || RAMCRC_BIN_RESCUE) {
+        // after k_bin_one: the guarded scatter (exits at once unless k_bin_one aborted)
         hipLaunchKernelGGL(k_bin_scatter<kMode>, dim3(bin_grid(c, d.n)), dim3(kThreads), 0, s, d,
-                           so, skip_large);
+                           so, skip_large, int(so.one));
         HIPCHK(hipGetLastError());
     }
     {
@@ -5770,6 +5835,7 @@ int ramcrc_ctx_debug_bins(ramcrc_ctx* c, uint64_t* host, uint64_t nwords, uint32
         for (int b = 0; b < kNB; b++) v.push_back(h.ctr[p].cursor[b]);
     for (int p = 0; p < 2; p++)
         for (int b = 0; b < kNB; b++) v.push_back(h.ctr[p].hist[b]);
+    v.push_back(h.rescues);
     for (uint64_t i = 0; i < nwords && i < v.size(); i++)
         host[i] = v[i];
     if (par_next)

@@ -304,6 +304,15 @@ class Context:
                                            _c.byref(par)), "ramcrc_ctx_debug_bins")
         return buf[:161], buf[161:483].reshape(2, 161), buf[483:].reshape(2, 161), par.value
 
+    def bin_rescues(self):
+        """One-launch binnings of this context that aborted (part of the grid
+        not dispatched in time) and completed through the two-launch path."""
+        buf = np.zeros(5 * 161 + 1, np.uint64)
+        par = _c.c_uint32(0)
+        _check(lib().ramcrc_ctx_debug_bins(self._h, _c.c_void_p(buf.ctypes.data), buf.size,
+                                           _c.byref(par)), "ramcrc_ctx_debug_bins")
+        return int(buf[-1])
+
     def set_option(self, option, value):
         """ramcrc_ctx_set_option (OPT_* above)."""
         _check(lib().ramcrc_ctx_set_option(self._h, int(option), int(value)), "ramcrc_ctx_set_option")
