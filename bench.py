@@ -412,12 +412,17 @@ def run_recovery(args, ranks):
     bad = int((gathered != expect).sum())
     bad_per_rank = ranks.gather_objects(bad)
     shard.close()
+    # The reference's CPU path beside the GPU line, at every N (rank 0, outside
+    # the timed region): intelCrc32C over the whole batch on this host's cores.
+    cpu = None
+    if ranks.rank == 0 and ranks.world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_segments(data.cpu().numpy(), seg, total, gathered, reps=args.cpu_reps)
     del data
     torch.cuda.empty_cache()
     ranks.barrier()
     t1 = None
-    if ranks.rank == 0 and ranks.world > 1 and not args.no_t1:
-        t1 = _recovery_t1(args, ranks, setup)
+    if ranks.rank == 0 and ranks.world > 1 and not (args.no_t1 and args.no_cpu_baseline):
+        t1, cpu = _recovery_t1(args, ranks, setup, gathered)
     ranks.barrier()
     setup.close()
     if ranks.rank != 0:
@@ -439,6 +444,7 @@ def run_recovery(args, ranks):
                    "segment_bytes": seg, "parallelism": f"shard{ranks.world}",
                    "exchange": "RCCL ncclAllGather of uint32 CRCs (libramcrc ramcrc_shard_segments)"},
         "roofline": roofline("k_chunks", count * seg, avg_ms, key),
+        "cpu_baseline": cpu,
         "bit_exact": all(b == 0 for b in bad_per_rank),
         "bit_exact_check": (f"all {total} gathered CRCs on each of the {ranks.world} ranks vs "
                             "each owner's host CRCs of its segments (libramcrc SSE4.2 path); "
@@ -465,29 +471,37 @@ def _host_segment_crcs(data, seg, count, batch=32, threads=8):
     return out
 
 
-def _recovery_t1(args, ranks, ctx):
-    """The whole C4 batch on rank 0's GPU alone (a 1-rank shard), same steps."""
+def _recovery_t1(args, ranks, ctx, gathered):
+    """The whole C4 batch built on rank 0's GPU: timed there alone (a 1-rank
+    shard, same steps; unless --no-t1) and, unless --no-cpu-baseline, copied to
+    the host for the reference CPU baseline, whose CRCs are compared with the
+    N-rank step's gathered ones.  Returns (t1 ms or None, cpu_baseline or None)."""
     import torch
     from ramcloud_amd import ramcrc
     seg = args.seg_mib * MiB
     total = args.nseg_total
     data = torch.empty(total * seg, dtype=torch.uint8, device="cuda")
     _fill_recovery_shard(ctx, data, seg, 0, total, args.value_len)
-    solo = ramcrc.Shard(uid=ramcrc.shard_unique_id(), nranks=1, rank=0, device=ranks.local)
-    out = torch.zeros(total, dtype=torch.int32, device="cuda")
-    step = lambda: solo.segments([data], seg, total, outs=[out])  # noqa: E731
-    for _ in range(args.warmup):
-        step()
-    solo.sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    solo.sync()
-    t1 = (time.perf_counter() - t0) / args.steps * 1e3
-    solo.close()
+    t1 = None
+    if not args.no_t1:
+        solo = ramcrc.Shard(uid=ramcrc.shard_unique_id(), nranks=1, rank=0, device=ranks.local)
+        out = torch.zeros(total, dtype=torch.int32, device="cuda")
+        step = lambda: solo.segments([data], seg, total, outs=[out])  # noqa: E731
+        for _ in range(args.warmup):
+            step()
+        solo.sync()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        solo.sync()
+        t1 = (time.perf_counter() - t0) / args.steps * 1e3
+        solo.close()
+    cpu = None
+    if not args.no_cpu_baseline:
+        cpu = cpu_baseline_segments(data.cpu().numpy(), seg, total, gathered, reps=args.cpu_reps)
     del data
     torch.cuda.empty_cache()
-    return t1
+    return t1, cpu
 
 
 def run_recovery_host_dry(args, ranks):
@@ -523,6 +537,15 @@ def run_recovery_host_dry(args, ranks):
     if ranks.rank != 0:
         return None
     crcs = box["full"].numpy().view(np.uint32)
+    cpu = None
+    if not args.no_cpu_baseline:
+        # as the GPU line: the reference's CPU path over the whole batch, rank 0
+        full = np.empty(total * seg, np.uint8)
+        for i in range(total):
+            s = full[i * seg:(i + 1) * seg]
+            s[:] = workloads.splitmix_bytes_np(workloads.SEGMENT_SEED + i, seg)
+            ramcrc.segment_fill_objects(s, args.value_len, first_key=i * per)
+        cpu = cpu_baseline_segments(full, seg, total, crcs, reps=args.cpu_reps)
     return {
         "metric": METRIC + " [host dry run: CPU plumbing test, not a GPU measurement]",
         "value": round(total * seg * args.steps / elapsed / 1e9, 4), "unit": "GB/s",
@@ -535,6 +558,7 @@ def run_recovery_host_dry(args, ranks):
                    "segment_bytes": seg, "value_len": args.value_len,
                    "parallelism": f"shard{ranks.world}", "exchange": "gloo all_gather (dry run)"},
         "dry_run": True,
+        "cpu_baseline": cpu,
         "crcs": [int(c) for c in crcs] if total <= 256 else None,
         "crc_of_crcs": ramcrc.crc32c(np.ascontiguousarray(crcs)),
     }
@@ -559,10 +583,9 @@ def run_entries(args, ranks):
     len_t = torch.from_numpy(lens.view(np.int64)).cuda()
     out = torch.zeros(lens.size, dtype=torch.int32, device="cuda")
     fn = ctx.entries if args.path == "entries" else ctx.batch
-    ordered = args.order == "log"
     torch.cuda.synchronize()
     ctx.set_timing(True)
-    elapsed = timed(args.steps, args.warmup, lambda: fn(data, off_t, len_t, out, ordered=ordered),
+    elapsed = timed(args.steps, args.warmup, lambda: fn(data, off_t, len_t, out),
                     torch.cuda.synchronize, ranks, on_start=ctx.scan_time)
     kernel_ms, _ = ctx.scan_time()
     ctx.set_timing(False)
@@ -574,10 +597,8 @@ def run_entries(args, ranks):
     cpu = None if args.no_cpu_baseline else cpu_baseline_entries(host, offs, lens, gpu)
     scan_ms = kernel_ms / args.steps
     mix = "fixed %d B" % args.entry_size if args.entry_size else "100B/1KiB/4KiB Zipf"
-    key = (f"c3_{lens.size}_{'mix' if not args.entry_size else args.entry_size}_{args.path}"
-           + ("_ordered" if ordered else ""))
-    kernel = ("k_stream (one pass over the log-ordered entries)" if ordered else
-              "k_entries (tiny + long phases)" if args.path == "entries" else "k_chunks+k_entries")
+    key = f"c3_{lens.size}_{'mix' if not args.entry_size else args.entry_size}_{args.path}"
+    kernel = "k_entries (tiny + long phases)" if args.path == "entries" else "k_chunks+k_entries"
     ctx.close()
     return {
         "metric": f"device-resident CRC32C GB/s over {lens.size} log entries ({mix})",
@@ -587,8 +608,6 @@ def run_entries(args, ranks):
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
         "config": {"workload": f"{lens.size} entries, {total} bytes per GPU (BASELINE config 3)",
                    "path": args.path,
-                   "order": ("log order (RAMCRC_ORDERED: sorted, non-overlapping, verified on the "
-                             "device in the timed region)" if ordered else "any (binned path)"),
                    "parallelism": f"replicas{ranks.world}" if ranks.world > 1 else "single",
                    "exchange": "none", "table_bytes_not_credited": 16 * lens.size},
         "roofline": dict(roofline(kernel, total, scan_ms, key),
@@ -813,11 +832,10 @@ def run_append(args, ranks):
     off_t = torch.from_numpy(offs.view(np.int64)).cuda()
     len_t = torch.from_numpy(lens.view(np.int64)).cuda()
     out = torch.zeros(lens.size, dtype=torch.int32, device="cuda")
-    ordered = args.order == "log"
     torch.cuda.synchronize()
     ctx.set_timing(True)
     elapsed = timed(args.steps, args.warmup,
-                    lambda: ctx.assemble_objects(data, off_t, len_t, out, ordered=ordered),
+                    lambda: ctx.assemble_objects(data, off_t, len_t, out),
                     torch.cuda.synchronize, ranks, on_start=ctx.scan_time)
     scan_ms, _ = ctx.scan_time()
     ctx.set_timing(False)
@@ -840,11 +858,8 @@ def run_append(args, ranks):
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-        "config": {"workload": f"{lens.size} objects, {total} bytes", "credited_bytes": credited,
-                   "order": ("log order (ramcrc_assemble_objects_ordered_device, verified on the "
-                             "device)" if ordered else "any (binned path)")},
-        "roofline": dict(roofline("k_stream (objects mode)" if ordered else "k_entries", credited,
-                                  scan_s * 1e3, f"append_{lens.size}_mix" + ("_ordered" if ordered else "")),
+        "config": {"workload": f"{lens.size} objects, {total} bytes", "credited_bytes": credited},
+        "roofline": dict(roofline("k_entries", credited, scan_s * 1e3, f"append_{lens.size}_mix"),
                          scan_ms_per_step=round(scan_s * 1e3, 4)),
         "cpu_baseline": cpu,
     }
@@ -932,9 +947,6 @@ def parse_args(argv=None):
                     help="replay: force log2 of the parallel walk's part bytes (0: chosen per batch)")
     ap.add_argument("--entries", type=int, default=1_000_000)
     ap.add_argument("--path", default="entries", choices=["entries", "batch"])
-    ap.add_argument("--order", default="any", choices=["log", "any"],
-                    help="entries config: log = RAMCRC_ORDERED stream pass (the entries are "
-                         "packed in log order); any = the binned path for arbitrary tables")
     ap.add_argument("--entry-size", type=int, default=0, help="fixed entry length (default: Zipf mix)")
     ap.add_argument("--exclude-size", type=int, default=0,
                     help="entries config: drop the entries of this size from the mix (A/B only)")

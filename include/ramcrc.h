@@ -47,30 +47,15 @@ enum {
                              binning whose grid is not all resident (other contexts'
                              kernels, preemption) falls back to the two-launch binning
                              inside the same call.  See ramcrc_ctx_check. */
-    RAMCRC_EPEER = -8,    /* multi-GPU shard: this rank's part of the step succeeded but
+    RAMCRC_EPEER = -8     /* multi-GPU shard: this rank's part of the step succeeded but
                              another rank's failed; that rank's segments read 0xFFFFFFFF */
-    RAMCRC_EORDER = -9    /* a RAMCRC_ORDERED batch was not in log order (entries overlap,
-                             are out of order, or leave a gap of 4 KiB or more between
-                             neighbours): nothing was written (see ramcrc_ctx_check) */
+    /* -9 was RAMCRC_EORDER of the ordered-stream batches, removed in round 5 */
 };
 
 /* Output flag: apply the final inversion (Crc32C::getResult, src/Crc32C.h:247).
  * Without it the raw running state (Crc32C::result, :259) is returned, which
  * callers use to keep chaining (src/LogDigest.cc:75-80, src/Segment.cc:677-681). */
 #define RAMCRC_FINALIZE 1u
-
-/* Input flag of ramcrc_batch_device / ramcrc_entries_device: the buffers are
- * log entries in log order -- sorted by offset, not overlapping, neighbours
- * less than 4 KiB apart (the bytes between them readable), as the entries of a
- * segment (src/Segment.cc:197-228), the objects a replay walks
- * (src/ObjectManager.cc:585-700) or a write batch appended in order
- * (src/ObjectManager.cc:1274-1297) lie.  The batch is then checksummed as one
- * byte stream in a single pass (every covered byte read once, entry ends
- * resolved on the fly) instead of entry by entry.  Results are identical.
- * The order is verified on the device; a batch that breaks it is refused
- * (nothing written, RAMCRC_EORDER from ramcrc_ctx_check).  Ignored when d_init
- * is not NULL (per-entry initial states take the general path). */
-#define RAMCRC_ORDERED 2u
 
 /* ---------------------------------------------------------------- host --- */
 
@@ -281,22 +266,6 @@ int ramcrc_verify_objects_device(ramcrc_ctx* ctx, const void* d_base, uint64_t s
                                  const uint64_t* d_n_entries, uint32_t* d_obj_crc,
                                  ramcrc_seg_status* d_status, void* stream);
 
-/* The same checks with the objects checksummed in one ordered pass over each
- * segment's bytes (the RAMCRC_ORDERED stream, spans per segment) instead of
- * object by object: every object's Object::computeChecksum and its
- * comparison with the stored checksum happen as the pass crosses the object's
- * end.  n_seg is the number of segments the walk covered.  The record table
- * must be the one ramcrc_segment_walk_device wrote: each segment's records
- * contiguous and in offset order (both walkers write them so); a table that
- * is not is refused (nothing checked, RAMCRC_EORDER from ramcrc_ctx_check)
- * and can be verified with ramcrc_verify_objects_device.  Results are
- * identical to ramcrc_verify_objects_device's. */
-int ramcrc_verify_objects_ordered_device(ramcrc_ctx* ctx, const void* d_base, uint64_t seg_stride,
-                                         uint64_t n_seg, const ramcrc_seg_entry* d_entries,
-                                         uint64_t entries_cap, const uint64_t* d_n_entries,
-                                         uint32_t* d_obj_crc, ramcrc_seg_status* d_status,
-                                         void* stream);
-
 /* Host append path (src/Segment.cc:197-228 with src/Object.cc:213-218):
  * appends LOG_ENTRY_TYPE_OBJ entries holding objects {tableId 0, key = 8-byte
  * counter from first_key, version 0, timestamp 0, value_len value bytes} to an
@@ -413,16 +382,6 @@ int ramcrc_shard_results(ramcrc_shard* shard, int k, uint32_t* h_out, uint64_t n
 int ramcrc_assemble_objects_device(ramcrc_ctx* ctx, void* d_base, const uint64_t* d_off,
                                    const uint64_t* d_len, uint32_t* d_out, uint64_t n,
                                    void* stream);
-
-/* The same for a write batch whose objects lie in log order (sorted by
- * offset, not overlapping, neighbours less than 4 KiB apart: packed as
- * AbstractLog::append lays them out, src/AbstractLog.cc:374-427): the
- * RAMCRC_ORDERED stream pass checksums all of them in one pass over the
- * batch's bytes.  Same results; a batch out of order is refused (nothing
- * checksummed or stamped, RAMCRC_EORDER from ramcrc_ctx_check). */
-int ramcrc_assemble_objects_ordered_device(ramcrc_ctx* ctx, void* d_base, const uint64_t* d_off,
-                                           const uint64_t* d_len, uint32_t* d_out, uint64_t n,
-                                           void* stream);
 
 /* The same for objects in host memory (a write batch still in its RPC
  * buffers): staged through pinned memory, CRCs computed on the GPU, each

@@ -20,7 +20,7 @@ LIB = os.path.join(LIBDIR, "libramcrc.so")
 ARCH = "gfx950"
 
 SOURCES = ["ramcrc_device.hip", "ramcrc_host.cc", "ramcrc_shard.hip", "ramcrc_fill.hip"]
-HEADERS = ["gf2.h", "walk_rules.h", "shard_plan.h", "stream.h"]
+HEADERS = ["gf2.h", "walk_rules.h", "shard_plan.h"]
 
 
 def hipcc():

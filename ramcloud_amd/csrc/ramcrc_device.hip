@@ -95,8 +95,7 @@ struct alignas(16) DeviceTables {
     uint32_t post[256 * 128 + 128];
     uint32_t xmeta[5 * 64 + 1];   // k_seg_walk: x^(8d), d = 0 .. 320 (one batch of metadata)
     uint32_t xbyte[4][256];       // x^(8 * b * 256^j): x^(8d) for any 32-bit d in 4 factors
-    alignas(16) OpTable xinv128;  // k_stream: X^-128 (an entry's value moved back from the step end)
-    alignas(16) uint32_t xff[132];   // k_stream: X^d(0xFFFFFFFF), d = 0 .. 128 (the initial state)
+    alignas(16) OpTable xinv128;  // tiny phase: X^-128 (a window sum moved back from the window end)
     // k_entries' long phase (group_fold, flush_batch, head and tail steps),
     // laid out as in LDS from kX4Off on, so one fill copies them all:
     struct alignas(16) LongTabs {
@@ -153,8 +152,6 @@ constexpr DeviceTables make_device_tables()
         for (int k = 0; k < 4; k++)
             for (uint32_t b = 0; b < 256; b++)
                 t.xinv128.t[k][b] = ramcrc::mulmod(b << (8 * k), c);
-        for (int dd = 0; dd <= 128; dd++)
-            t.xff[dd] = ramcrc::mulmod(0xFFFFFFFFu, ramcrc::xpow8(uint64_t(dd)));
     }
     t.lt.x4 = t.comb[0];
     t.lt.x16 = t.comb[1];
@@ -3298,8 +3295,6 @@ __global__ __launch_bounds__(kThreads) void k_plan_scan(Plan pl)
         pl.group_pref[pl.ngroups] = carry_s;
 }
 
-#include "stream.h"
-
 // Test hook (RAMCRC_OPT_TEST_DIRTY_BINS): corrupt the histogram of a binning
 // sequence between its count and scatter passes, as a stale histogram would.
 __global__ void k_test_dirty_bins(BinTable* bt, uint32_t par, uint32_t bin, uint32_t add)
@@ -3312,7 +3307,7 @@ __global__ void k_test_dirty_bins(BinTable* bt, uint32_t par, uint32_t bin, uint
 // to status[1] for the host to read.
 __global__ void k_status_take(uint32_t* status)
 {
-    status[1] = atomicAnd(status, ~(kStatusSticky | kStatusBins | kStatusOrder));
+    status[1] = atomicAnd(status, ~(kStatusSticky | kStatusBins));
 }
 
 // ------------------------------------------------------------ host side
@@ -3400,13 +3395,6 @@ struct ramcrc_ctx {
     uint64_t walk_pool_used_cap = 0;
     bool serial_walk = false;   // RAMCRC_OPT_SERIAL_WALK
     uint32_t walk_pshift = 0;   // RAMCRC_OPT_WALK_PART_SHIFT; 0: kPartShift
-    // ordered-stream scratch (k_stream*): 4 words per span + the refusal word
-    uint32_t* stream_scr = nullptr;
-    uint64_t stream_scr_cap = 0;
-    uint32_t stream_seq = 0;
-    uint32_t* stream_bad = nullptr;   // the refusal word of ordered launches (own allocation)
-    unsigned long long* rec_first = nullptr;   // records mode: seq << 32 | first record, per segment
-    uint64_t rec_first_cap = 0;
     // benchmark timing of the scan kernels
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_used, ev_free;
@@ -3682,139 +3670,6 @@ int launch_planned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, const uint3
     return bin_finish<kMode>(c, d, s, 1, so);
 }
 
-// Scratch of the ordered launches.  The refusal word has an allocation of its
-// own and the sequence number only grows, so no word an earlier launch left
-// (of any layout) can read as this launch's refusal or segment index.
-int reserve_stream(ramcrc_ctx* c, uint64_t words)
-{
-    if (!c->stream_bad) {
-        if (hipMalloc(reinterpret_cast<void**>(&c->stream_bad), 16) != hipSuccess) {
-            c->stream_bad = nullptr;
-            return RAMCRC_ENOMEM;
-        }
-        HIPCHK(hipMemset(c->stream_bad, 0, 16));
-    }
-    if (c->stream_scr_cap < words)
-        return grow_device(reinterpret_cast<void**>(&c->stream_scr), &c->stream_scr_cap, words,
-                           sizeof(uint32_t));
-    return RAMCRC_OK;
-}
-
-uint32_t next_stream_seq(ramcrc_ctx* c)
-{
-    if (++c->stream_seq == 0)
-        ++c->stream_seq;   // 0 is the word's initial value
-    return c->stream_seq;
-}
-
-// Ordered batch (RAMCRC_ORDERED): k_stream_prep -> k_stream -> k_stream_fix
-// (stream.h).  Every launch gets a new sequence number, so a refusal word
-// left by an earlier launch never stops a later one.
-int launch_stream(ramcrc_ctx* c, const uint8_t* base, const uint64_t* off, const uint64_t* len,
-                  uint32_t* out, uint64_t n, uint32_t flags, hipStream_t s, bool objects = false)
-{
-    if (n >= (1ull << 32) - 1)
-        return RAMCRC_EINVAL;   // 32-bit entry indices
-    const uint32_t nspan = uint32_t(c->ncu) * kStreamGroups;
-    int rc = reserve_stream(c, 4ull * nspan);
-    if (rc)
-        return rc;
-    StreamDesc d{};
-    d.base = base;
-    d.off = off;
-    d.len = len;
-    d.n = n;
-    d.out = out;
-    d.flags = flags;
-    d.obj = objects ? 1u : 0u;
-    d.nspan = nspan;
-    d.seq = next_stream_seq(c);
-    d.first_ev = c->stream_scr;
-    d.span_t = c->stream_scr + nspan;
-    d.xe_val = c->stream_scr + 2 * uint64_t(nspan);
-    d.xe_idx = c->stream_scr + 3 * uint64_t(nspan);
-    d.bad_seq = c->stream_bad;
-    d.status = c->status;
-    uint64_t pg = (n + 255) / 256;
-    if (pg > uint64_t(c->ncu) * 8)
-        pg = uint64_t(c->ncu) * 8;
-    hipLaunchKernelGGL(k_stream_prep, dim3(pg), dim3(256), 0, s, d);
-    HIPCHK(hipGetLastError());
-    {
-        ScanTimer t(c, s);
-        t.launch(k_stream<false>, dim3(c->ncu), dim3(kStreamWaves * kWaveSize), d);
-    }
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_stream_fix<false>, dim3((nspan + 255) / 256), dim3(256), 0, s, d);
-    HIPCHK(hipGetLastError());
-    return RAMCRC_OK;
-}
-
-// Records mode (ramcrc_verify_objects_device): the objects of a walk's record
-// table, segment by segment.  spr spans per segment (a multiple of 8) so that
-// about one span per group of a full grid; more segments than that run as
-// more workgroups.
-int launch_stream_records(ramcrc_ctx* c, const BatchDesc& bd, uint64_t nseg, hipStream_t s)
-{
-    if (bd.n >= (1ull << 32) - 1 || nseg >= (1ull << 32))
-        return RAMCRC_EINVAL;
-    const uint64_t full = uint64_t(c->ncu) * kStreamGroups;
-    uint64_t spr = full / (nseg ? nseg : 1) / 8 * 8;
-    if (spr < 8)
-        spr = 8;
-    if (spr > 4096)
-        spr = 4096;
-    const uint64_t nspan = nseg * spr;
-    int rc = reserve_stream(c, 4 * nspan);
-    if (rc)
-        return rc;
-    if (c->rec_first_cap < nseg) {
-        rc = grow_device(reinterpret_cast<void**>(&c->rec_first), &c->rec_first_cap, nseg,
-                         sizeof(unsigned long long));
-        if (rc)
-            return rc;
-        HIPCHK(hipMemset(c->rec_first, 0, c->rec_first_cap * sizeof(unsigned long long)));
-    }
-    StreamDesc d{};
-    d.base = bd.base;
-    d.n = bd.n;
-    d.out = bd.out;
-    d.flags = RAMCRC_FINALIZE;
-    d.nspan = uint32_t(nspan);
-    d.seq = next_stream_seq(c);
-    d.first_ev = c->stream_scr;
-    d.span_t = c->stream_scr + nspan;
-    d.xe_val = c->stream_scr + 2 * nspan;
-    d.xe_idx = c->stream_scr + 3 * nspan;
-    d.bad_seq = c->stream_bad;
-    d.seg_first = c->rec_first;
-    d.status = c->status;
-    d.rec = bd.rec;
-    d.n_dev = bd.n_dev;
-    d.vstat = bd.vstat;
-    d.stride = bd.seg_bytes;
-    d.nseg = nseg;
-    d.spr = uint32_t(spr);
-    uint64_t pg = (bd.n + 255) / 256;
-    if (pg > uint64_t(c->ncu) * 8)
-        pg = uint64_t(c->ncu) * 8;
-    if (pg == 0)
-        pg = 1;
-    hipLaunchKernelGGL(k_stream_rprep, dim3(pg), dim3(256), 0, s, d);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_stream_rprep2, dim3(pg), dim3(256), 0, s, d);
-    HIPCHK(hipGetLastError());
-    {
-        ScanTimer t(c, s);
-        t.launch(k_stream<true>, dim3(nspan / kStreamGroups + (nspan % kStreamGroups ? 1 : 0)),
-                 dim3(kStreamWaves * kWaveSize), d);
-    }
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_stream_fix<true>, dim3((nspan + 255) / 256), dim3(256), 0, s, d);
-    HIPCHK(hipGetLastError());
-    return RAMCRC_OK;
-}
-
 // ------------------------------------------------------------ segment walk
 // Segment::checkMetadataIntegrity (src/Segment.cc:758-800) on the device: one
 // wavefront per segment.  The walk is a pointer chase through length-prefixed
@@ -3908,8 +3763,7 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
         const ramcrc_seg_cert cert = w.certs[seg];
         // Two passes: the first counts the records, one atomic allocates them,
         // the second writes them -- so every segment's records are contiguous
-        // and in offset order (the parallel walk's are too), which the ordered
-        // object scan relies on (stream.h, records mode).
+        // and in offset order (the parallel walk's are too).
         unsigned long long rbase = 0, rdone = 0, rtotal = 0;
         for (int pass = 0; pass < 2; pass++) {
         uint32_t pos = 0, crc = 0xFFFFFFFFu, count = 0, flags = 0;
@@ -5431,28 +5285,24 @@ __device__ __forceinline__ uint32_t le32_g(const gu8* p)
 }
 
 
-// skip_objs: every readable object was checked by the ordered scan
-// (k_stream<true>); bad_seq (nullable) == seq: that scan was refused, and
-// nothing is checked here either.
 // nother (nullable): the binning count of records this kernel has work for
 // (replay_other); 0 ends the launch at once.  Grid-stride over the records.
 __device__ __forceinline__ void obj_compare_one(const BatchDesc& d, ramcrc_seg_status* status,
-                                                int skip_objs, uint64_t i);
+                                                uint64_t i);
 
 __global__ __launch_bounds__(256) void k_obj_compare(BatchDesc d, ramcrc_seg_status* status,
-                                                     int skip_objs, const uint32_t* bad_seq,
-                                                     uint32_t seq, const uint32_t* nother)
+                                                     const uint32_t* nother)
 {
-    if ((bad_seq && *bad_seq == seq) || (nother && *nother == 0))
+    if (nother && *nother == 0)
         return;
     const uint64_t n = entry_count<kRecords>(d);
     for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
          i += uint64_t(gridDim.x) * blockDim.x)
-        obj_compare_one(d, status, skip_objs, i);
+        obj_compare_one(d, status, i);
 }
 
 __device__ __forceinline__ void obj_compare_one(const BatchDesc& d, ramcrc_seg_status* status,
-                                                int skip_objs, uint64_t i)
+                                                uint64_t i)
 {
     const u32x4 r = d.rec[i];
     const uint32_t type = r.w & 0x3f;
@@ -5460,9 +5310,8 @@ __device__ __forceinline__ void obj_compare_one(const BatchDesc& d, ramcrc_seg_s
     if (hdr == 0)
         return;
     const bool readable = r.z >= hdr && !(r.w & kRecOverlong);
-    if (d.vstat && type == RAMCRC_LOG_ENTRY_TYPE_OBJ && readable &&
-        (skip_objs || !is_large(uint64_t(r.z) - 4)))
-        return;   // compared beside the scan (k_stream: all; k_entries: below the 64 KiB split)
+    if (d.vstat && type == RAMCRC_LOG_ENTRY_TYPE_OBJ && readable && !is_large(uint64_t(r.z) - 4))
+        return;   // compared beside the scan (k_entries, below the 64 KiB split)
     const uint64_t payload = reinterpret_cast<uint64_t>(d.base) + uint64_t(r.x) * d.seg_bytes +
                              r.y + 1 + ((r.w >> 6) & 3) + 1;
     const gu8* p = reinterpret_cast<const gu8*>(payload);
@@ -5519,12 +5368,10 @@ __device__ __forceinline__ void obj_compare_one(const BatchDesc& d, ramcrc_seg_s
 // kernels left in d.out[i], stored little-endian into the object's first 4
 // bytes (which no object's checksum range covers).  Byte stores: objects are
 // packed back to back in a log, so headers are unaligned.
-// bad_seq (nullable): an ordered launch's refusal word; when it holds seq the
-// scan wrote nothing, and neither does the stamp.
-__global__ __launch_bounds__(256) void k_obj_stamp(BatchDesc d, const uint32_t* bad_seq, uint32_t seq)
+__global__ __launch_bounds__(256) void k_obj_stamp(BatchDesc d)
 {
     const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= d.n || (bad_seq && *bad_seq == seq))
+    if (i >= d.n)
         return;
     if (d.len[i] < kObjHeaderBytes) {
         d.out[i] = 0;
@@ -5595,7 +5442,6 @@ const char* ramcrc_strerror(int code)
     case RAMCRC_EREFUSED: return "launch refused: chunk scratch too small (ramcrc_ctx_reserve)";
     case RAMCRC_EINTERNAL: return "launch refused: inconsistent small-entry bin layout";
     case RAMCRC_EPEER: return "another rank of the shard failed this step";
-    case RAMCRC_EORDER: return "ordered batch refused: entries overlap, are out of order or leave a gap of 4 KiB or more";
     default: return "unknown error";
     }
 }
@@ -5696,9 +5542,6 @@ int ramcrc_ctx_destroy(ramcrc_ctx* c)
     if (c->walk_pool_owner) (void)hipFree(c->walk_pool_owner);
     if (c->walk_blocks) (void)hipFree(c->walk_blocks);
     if (c->walk_pool_used) (void)hipFree(c->walk_pool_used);
-    if (c->stream_scr) (void)hipFree(c->stream_scr);
-    if (c->stream_bad) (void)hipFree(c->stream_bad);
-    if (c->rec_first) (void)hipFree(c->rec_first);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -5872,8 +5715,6 @@ int ramcrc_ctx_check(ramcrc_ctx* c, void* stream)
     HIPCHK(hipMemcpy(&st, c->status + 1, sizeof(uint32_t), hipMemcpyDeviceToHost));
     if (st & kStatusBins)
         return RAMCRC_EINTERNAL;
-    if (st & kStatusOrder)
-        return RAMCRC_EORDER;
     return (st & kStatusSticky) ? RAMCRC_EREFUSED : RAMCRC_OK;
 }
 
@@ -5952,9 +5793,6 @@ int ramcrc_batch_device(ramcrc_ctx* c, const void* d_base, const uint64_t* d_off
     d.init = d_init;
     d.out = d_out;
     d.flags = flags;
-    if ((flags & RAMCRC_ORDERED) && !d_init)
-        return launch_stream(c, d.base, d_off, d_len, d_out, n, flags,
-                             reinterpret_cast<hipStream_t>(stream));
     return launch_planned<kTable>(c, d, reinterpret_cast<hipStream_t>(stream));
 }
 
@@ -5978,8 +5816,6 @@ int ramcrc_entries_device(ramcrc_ctx* c, const void* d_base, const uint64_t* d_o
     d.init = d_init;
     d.out = d_out;
     d.flags = flags;
-    if ((flags & RAMCRC_ORDERED) && !d_init)
-        return launch_stream(c, d.base, d_off, d_len, d_out, n, flags, s);
     return launch_binned<kTable>(c, d, s, 0);
 }
 
@@ -6332,47 +6168,7 @@ int ramcrc_verify_objects_device(ramcrc_ctx* c, const void* d_base, uint64_t seg
         return rc;
     uint64_t grid = (entries_cap + 255) / 256;
     grid = grid < uint64_t(16) * c->ncu ? grid : uint64_t(16) * c->ncu;
-    hipLaunchKernelGGL(k_obj_compare, dim3(grid), dim3(256), 0, s, d, d_status, 0,
-                       static_cast<const uint32_t*>(nullptr), 0u, nother);
-    HIPCHK(hipGetLastError());
-    return RAMCRC_OK;
-}
-
-int ramcrc_verify_objects_ordered_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride,
-                                         uint64_t n_seg, const ramcrc_seg_entry* d_entries,
-                                         uint64_t entries_cap, const uint64_t* d_n_entries,
-                                         uint32_t* d_obj_crc, ramcrc_seg_status* d_status,
-                                         void* stream)
-{
-    if (!c)
-        return RAMCRC_EINVAL;
-    if (entries_cap == 0 || n_seg == 0)
-        return RAMCRC_OK;
-    if (!d_base || !d_entries || !d_n_entries || !d_obj_crc || !d_status || (seg_stride & 15) ||
-        (reinterpret_cast<uintptr_t>(d_base) & 15))
-        return RAMCRC_EINVAL;
-    std::lock_guard<std::recursive_mutex> lk(c->mu);
-    DeviceGuard g(c->device);
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    BatchDesc d{};
-    d.base = static_cast<const uint8_t*>(d_base);
-    d.seg_bytes = seg_stride;
-    d.n = entries_cap;
-    d.vstat = d_status;
-    d.rec = reinterpret_cast<const u32x4*>(d_entries);
-    d.n_dev = d_n_entries;
-    d.seg_status = reinterpret_cast<const u32x4*>(d_status);
-    d.out = d_obj_crc;
-    d.flags = RAMCRC_FINALIZE;
-    int rc = launch_stream_records(c, d, n_seg, s);
-    if (rc)
-        return rc;
-    // the other replayed types (and nothing when the scan was refused: the
-    // compare would read object CRCs that were never written)
-    const uint64_t grid = (entries_cap + 255) / 256;
-    hipLaunchKernelGGL(k_obj_compare, dim3(grid), dim3(256), 0, s, d, d_status, 1,
-                       static_cast<const uint32_t*>(c->stream_bad), c->stream_seq,
-                       static_cast<const uint32_t*>(nullptr));
+    hipLaunchKernelGGL(k_obj_compare, dim3(grid), dim3(256), 0, s, d, d_status, nother);
     HIPCHK(hipGetLastError());
     return RAMCRC_OK;
 }
@@ -6409,43 +6205,7 @@ int ramcrc_assemble_objects_device(ramcrc_ctx* c, void* d_base, const uint64_t* 
     rc = launch_planned<kObjects>(c, d, s);
     if (rc)
         return rc;
-    hipLaunchKernelGGL(k_obj_stamp, dim3((n + 255) / 256), dim3(256), 0, s, d,
-                       static_cast<const uint32_t*>(nullptr), 0u);
-    HIPCHK(hipGetLastError());
-    return RAMCRC_OK;
-}
-
-int ramcrc_assemble_objects_ordered_device(ramcrc_ctx* c, void* d_base, const uint64_t* d_off,
-                                           const uint64_t* d_len, uint32_t* d_out, uint64_t n,
-                                           void* stream)
-{
-    if (n == 0)
-        return c ? RAMCRC_OK : RAMCRC_EINVAL;
-    if (!c || !d_base || !d_off || !d_len)
-        return RAMCRC_EINVAL;
-    std::lock_guard<std::recursive_mutex> lk(c->mu);
-    DeviceGuard g(c->device);
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (!d_out) {
-        int rc = grow_device(reinterpret_cast<void**>(&c->obj_out), &c->obj_out_cap, n,
-                             sizeof(uint32_t));
-        if (rc)
-            return rc;
-        d_out = c->obj_out;
-    }
-    int rc = launch_stream(c, static_cast<const uint8_t*>(d_base), d_off, d_len, d_out, n,
-                           RAMCRC_FINALIZE, s, true);
-    if (rc)
-        return rc;
-    BatchDesc d{};
-    d.base = static_cast<const uint8_t*>(d_base);
-    d.off = d_off;
-    d.len = d_len;
-    d.n = n;
-    d.out = d_out;
-    d.flags = RAMCRC_FINALIZE;
-    hipLaunchKernelGGL(k_obj_stamp, dim3((n + 255) / 256), dim3(256), 0, s, d,
-                       static_cast<const uint32_t*>(c->stream_bad), c->stream_seq);
+    hipLaunchKernelGGL(k_obj_stamp, dim3((n + 255) / 256), dim3(256), 0, s, d);
     HIPCHK(hipGetLastError());
     return RAMCRC_OK;
 }

@@ -130,6 +130,7 @@ struct Local {
     uint64_t last_nseg = 0;
     bool last_internal = false;
     int failed = 0;               // a step's failure after its collective was enqueued
+    bool step_status = false;     // the last step exchanged status words (nseg > 0)
 };
 
 struct DevGuard {
@@ -208,9 +209,11 @@ struct StepOps {
     uint32_t flags;
 
     uint32_t* recv(int k, bool caller) { return caller ? d_all[k] : sh->local[k].gather; }
+    // Every argument a rank can get wrong is checked here, inside the step, so
+    // that the rank still joins the collectives (shard_plan.h's liveness rule).
     int check(int k, uint64_t lo, uint64_t hi)
     {
-        if (hi > lo && !d_shard[k])
+        if (hi > lo && (!d_shard || !d_shard[k] || seg_bytes == 0))
             return RAMCRC_EINVAL;
         if (d_all && !d_all[k])
             return RAMCRC_EINVAL;
@@ -480,7 +483,9 @@ int ramcrc_shard_info(const ramcrc_shard* sh, int k, int* rank, int* device, voi
 int ramcrc_shard_segments(ramcrc_shard* sh, const void* const* d_shard, uint64_t seg_bytes,
                           uint64_t nseg, uint32_t* const* d_all, uint32_t flags)
 {
-    if (!sh || !d_shard || seg_bytes == 0)
+    // (only a missing handle returns here: a null d_shard or seg_bytes == 0
+    // fail inside the step, StepOps::check, which still joins the collectives)
+    if (!sh)
         return RAMCRC_EINVAL;
     const Rccl* r = rccl();
     if (!r)
@@ -498,6 +503,10 @@ int ramcrc_shard_segments(ramcrc_shard* sh, const void* const* d_shard, uint64_t
     for (Local& l : sh->local) {
         l.last_nseg = rc ? 0 : nseg;
         l.last_internal = !d_all;
+        // an empty step exchanges nothing (run_step returns before any
+        // collective): the status words still on the device are an older
+        // step's and must not be reported for this one
+        l.step_status = nseg != 0;
     }
     return rc;
 }
@@ -509,9 +518,13 @@ int ramcrc_shard_sync(ramcrc_shard* sh)
     const Rccl* r = rccl();
     for (Local& l : sh->local) {
         DevGuard g(l.device);
-        // every rank's status word of the last exchange (shard_plan.h)
-        HIPCHK_S(hipMemcpyAsync(l.h_status, l.status, size_t(sh->nranks) * sizeof(uint32_t),
-                                hipMemcpyDeviceToHost, l.stream));
+        // every rank's status word of the last exchange (shard_plan.h); none
+        // for an empty step
+        if (l.step_status)
+            HIPCHK_S(hipMemcpyAsync(l.h_status, l.status, size_t(sh->nranks) * sizeof(uint32_t),
+                                    hipMemcpyDeviceToHost, l.stream));
+        else
+            memset(l.h_status, 0, size_t(sh->nranks) * sizeof(uint32_t));
         HIPCHK_S(hipStreamSynchronize(l.stream));
         if (r && l.comm) {
             ncclResult_t ae = ncclSuccess;

@@ -18,18 +18,15 @@ _c = ctypes
 _lib = None
 
 FINALIZE = 1
-ORDERED = 2   # RAMCRC_ORDERED: the batch is log entries in log order
 
 _ERRORS = {0: "ok", -1: "invalid argument", -2: "out of memory", -3: "HIP error",
            -4: "no usable device", -5: "RCCL error", -6: "launch refused (scratch too small)",
            -7: "launch refused (inconsistent bin layout)",
-           -8: "another shard rank failed",
-           -9: "ordered batch refused (entries not in log order)"}
+           -8: "another shard rank failed"}
 
 ENOMEM = -2
 EINTERNAL = -7
 EPEER = -8
-EORDER = -9
 
 # ramcrc_ctx_set_option options (include/ramcrc.h)
 OPT_SERIAL_WALK = 1
@@ -83,12 +80,10 @@ def lib():
         "ramcrc_stream_host": (i32, [vp, vp, u64, u64, vp, u32, i32, i32]),
         "ramcrc_segment_walk_device": (i32, [vp, vp, u64, u32, u64, vp, vp, vp, u64, vp, vp]),
         "ramcrc_verify_objects_device": (i32, [vp, vp, u64, vp, u64, vp, vp, vp, vp]),
-        "ramcrc_verify_objects_ordered_device": (i32, [vp, vp, u64, u64, vp, u64, vp, vp, vp, vp]),
         "ramcrc_segments_certify_device": (i32, [vp, vp, u64, u32, u64, vp, vp, vp, vp]),
         "ramcrc_segment_fill_objects": (i32, [vp, u32, u32, u64, _c.POINTER(u32), vp]),
         "ramcrc_assemble_objects_device": (i32, [vp, vp, vp, vp, vp, u64, vp]),
         "ramcrc_assemble_objects_host": (i32, [vp, vp, vp, u64]),
-        "ramcrc_assemble_objects_ordered_device": (i32, [vp, vp, vp, vp, vp, u64, vp]),
         "ramcrc_ctx_set_timing": (i32, [vp, i32]),
         "ramcrc_ctx_scan_time": (i32, [vp, _c.POINTER(_c.c_double), _c.POINTER(u64)]),
         "ramcrc_ctx_status": (i32, [vp, _c.POINTER(u32)]),
@@ -333,18 +328,17 @@ class Context:
         _check(rc, "ramcrc_segments_device")
         return out
 
-    def batch(self, data, off, length, out, init=None, finalize=True, stream=None, ordered=False):
-        """ordered=True: RAMCRC_ORDERED (entries in log order; one stream pass)."""
+    def batch(self, data, off, length, out, init=None, finalize=True, stream=None):
         n = off.numel()
-        fl = (FINALIZE if finalize else 0) | (ORDERED if ordered else 0)
+        fl = FINALIZE if finalize else 0
         rc = lib().ramcrc_batch_device(self._h, _ptr(data), _ptr(off), _ptr(length), _ptr(init),
                                        _ptr(out), n, fl, _stream(stream))
         _check(rc, "ramcrc_batch_device")
         return out
 
-    def entries(self, data, off, length, out, init=None, finalize=True, stream=None, ordered=False):
+    def entries(self, data, off, length, out, init=None, finalize=True, stream=None):
         n = off.numel()
-        fl = (FINALIZE if finalize else 0) | (ORDERED if ordered else 0)
+        fl = FINALIZE if finalize else 0
         rc = lib().ramcrc_entries_device(self._h, _ptr(data), _ptr(off), _ptr(length), _ptr(init),
                                          _ptr(out), n, fl, _stream(stream))
         _check(rc, "ramcrc_entries_device")
@@ -372,17 +366,8 @@ class Context:
         _check(rc, "ramcrc_segments_certify_device")
         return certs
 
-    def verify_objects(self, data, seg_stride, entries, n_entries, obj_crc, status, stream=None,
-                       nseg=None):
-        """Object::computeChecksum + comparison for every object record of a walk.
-        nseg given: the ordered pass over each segment
-        (ramcrc_verify_objects_ordered_device); else object by object."""
-        if nseg is not None:
-            rc = lib().ramcrc_verify_objects_ordered_device(
-                self._h, _ptr(data), seg_stride, int(nseg), _ptr(entries), entries.shape[0],
-                _ptr(n_entries), _ptr(obj_crc), _ptr(status), _stream(stream))
-            _check(rc, "ramcrc_verify_objects_ordered_device")
-            return status
+    def verify_objects(self, data, seg_stride, entries, n_entries, obj_crc, status, stream=None):
+        """Object::computeChecksum + comparison for every object record of a walk."""
         rc = lib().ramcrc_verify_objects_device(self._h, _ptr(data), seg_stride, _ptr(entries),
                                                 entries.shape[0], _ptr(n_entries), _ptr(obj_crc),
                                                 _ptr(status), _stream(stream))
@@ -402,17 +387,14 @@ class Context:
         _check(rc, "ramcrc_segment_fill_objects_device")
         return per.value, int(cert[0]), int(cert[1])
 
-    def assemble_objects(self, data, off, length, out=None, stream=None, ordered=False):
+    def assemble_objects(self, data, off, length, out=None, stream=None):
         """Object::assembleForLog's checksum for serialized objects in `data`
         (uint8 CUDA tensor, modified in place): header.checksum of object i
-        (bytes [off[i], off[i]+4)) = Crc32C over bytes [4, length[i]).
-        ordered=True: the objects lie in log order (one stream pass)."""
+        (bytes [off[i], off[i]+4)) = Crc32C over bytes [4, length[i])."""
         n = off.numel()
-        fn = (lib().ramcrc_assemble_objects_ordered_device if ordered
-              else lib().ramcrc_assemble_objects_device)
-        rc = fn(self._h, _ptr(data), _ptr(off), _ptr(length), _ptr(out), n, _stream(stream))
-        _check(rc, "ramcrc_assemble_objects_ordered_device" if ordered
-               else "ramcrc_assemble_objects_device")
+        rc = lib().ramcrc_assemble_objects_device(self._h, _ptr(data), _ptr(off), _ptr(length),
+                                                  _ptr(out), n, _stream(stream))
+        _check(rc, "ramcrc_assemble_objects_device")
         return out
 
     def assemble_objects_host(self, objects):

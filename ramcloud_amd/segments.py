@@ -101,12 +101,8 @@ class RecoveryVerify:
     tombstone and safe-version checks) after both
     kernels ran on the current stream."""
 
-    def __init__(self, ctx, nseg, capacity, stride=None, entries_cap=None, min_entry=None,
-                 ordered=False):
+    def __init__(self, ctx, nseg, capacity, stride=None, entries_cap=None, min_entry=None):
         self.ctx = ctx
-        # ordered: objects checked in one pass over each segment
-        # (ramcrc_verify_objects_ordered_device); False: object by object
-        self.ordered = ordered
         self.nseg = nseg
         self.capacity = capacity
         self.stride = capacity if stride is None else stride
@@ -146,8 +142,7 @@ class RecoveryVerify:
 
     def verify_objects(self, d_segments, stream=None):
         self.ctx.verify_objects(d_segments, self.stride, self.entries, self.n_entries,
-                                self.obj_crc, self.status, stream=stream,
-                                nseg=self.nseg if self.ordered else None)
+                                self.obj_crc, self.status, stream=stream)
         return self.status
 
     def verify(self, d_segments, d_certs, stream=None, check=False):

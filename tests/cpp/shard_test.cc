@@ -145,6 +145,21 @@ gpu(uint64_t nseg, uint64_t seg_bytes)
         EXPECT(ramcrc_shard_results(raw, 0, rawv.data(), nseg) == RAMCRC_OK);
         for (uint64_t i = 0; i < nseg; i++)
             EXPECT(rawv[i] == ~all[i]);
+        // a rank's bad arguments fail inside the step (it still joins the
+        // collectives): no shard pointers, then a zero segment size
+        EXPECT(ramcrc_shard_segments(raw, NULL, seg_bytes, nseg, NULL, 0) == RAMCRC_EINVAL);
+        EXPECT(ramcrc_shard_sync(raw) == RAMCRC_EINVAL);
+        EXPECT(ramcrc_shard_segments(raw, &shards[0], 0, nseg, NULL, 0) == RAMCRC_EINVAL);
+        EXPECT(ramcrc_shard_sync(raw) == RAMCRC_EINVAL);
+        // an empty step after a failed one reports nothing of the failed one
+        EXPECT(ramcrc_shard_segments(raw, &shards[0], seg_bytes, 0, NULL, 0) == RAMCRC_OK);
+        EXPECT(ramcrc_shard_sync(raw) == RAMCRC_OK);
+        // and the next real step is exact again
+        EXPECT(ramcrc_shard_segments(raw, &shards[0], seg_bytes, nseg, NULL, RAMCRC_FINALIZE) ==
+               RAMCRC_OK);
+        EXPECT(ramcrc_shard_sync(raw) == RAMCRC_OK);
+        EXPECT(ramcrc_shard_results(raw, 0, rawv.data(), nseg) == RAMCRC_OK);
+        EXPECT(rawv == all);
         ramcrc_shard_destroy(raw);
     }
     if (ndev == 1) {

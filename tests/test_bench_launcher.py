@@ -41,6 +41,10 @@ def test_bench_spawns_ranks_and_gathers(oracle_mod, ramcrc):
         ramcrc.segment_fill_objects(s, vlen, first_key=i * per)
         want.append(oracle_mod.crc32c(s))
     assert line["crcs"] == want
+    # the reference CPU baseline rides on the N > 1 line too (rank 0, whole batch)
+    cpu = line["cpu_baseline"]
+    assert cpu["bit_exact_vs_gpu"] is True and cpu["cores"] >= 1 and cpu["value"] > 0
+    assert cpu["kind"] in ("reference", "port")
 
 
 def test_bench_refuses_world_mismatch():

@@ -16,7 +16,7 @@ def _sorted(table, extra=None):
     return table[order], (None if extra is None else extra[order])
 
 
-def _run(ramcrc, buf, certs, nseg, cap, entries_cap, serial=False, part_shift=0, ordered=False):
+def _run(ramcrc, buf, certs, nseg, cap, entries_cap, serial=False, part_shift=0):
     import torch
 
     ctx = ramcrc.Context(0)
@@ -26,7 +26,7 @@ def _run(ramcrc, buf, certs, nseg, cap, entries_cap, serial=False, part_shift=0,
         ctx.set_walk_part_shift(part_shift)
     d = torch.from_numpy(buf).cuda()
     dc = torch.from_numpy(np.ascontiguousarray(certs).view(np.int32)).cuda()
-    rv = segments.RecoveryVerify(ctx, nseg, cap, entries_cap=entries_cap, ordered=ordered)
+    rv = segments.RecoveryVerify(ctx, nseg, cap, entries_cap=entries_cap)
     st = rv.verify(d, dc)
     torch.cuda.synchronize()
     n = int(rv.n_entries.item())
@@ -37,21 +37,18 @@ def _run(ramcrc, buf, certs, nseg, cap, entries_cap, serial=False, part_shift=0,
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("ordered", [False, True], ids=["by_object", "ordered"])
 @pytest.mark.parametrize("serial", [False, True], ids=["parallel_walk", "serial_walk"])
-def test_walk_verify_damage_batch(ramcrc, oracle_mod, serial, ordered):
+def test_walk_verify_damage_batch(ramcrc, oracle_mod, serial):
     """Clean segments of value lengths 0 .. 200000 (entries larger than the
     parallel walk's 64 KiB parts included), flipped values and checksums, bad
     and short certificates, overruns, a uint32_t offset wrap, a cycle, an
     empty segment, non-object and short-object entries, a certificate past
     the last entry: every status, record and object CRC equals the oracle's,
-    with the parallel and the serial walker, objects verified one by one
-    (binned) or in one ordered pass per segment (k_stream records mode)."""
+    with the parallel and the serial walker."""
     buf, certs, cases = segment_cases.build_batch(oracle_mod)
     nseg, cap = len(cases), segment_cases.CAPACITY
     exp_status, exp_table, exp_crc = segment_cases.oracle_walk(oracle_mod, buf, certs, nseg)
-    status, n, table, crc = _run(ramcrc, buf, certs, nseg, cap, nseg * (cap + 1), serial,
-                                 ordered=ordered)
+    status, n, table, crc = _run(ramcrc, buf, certs, nseg, cap, nseg * (cap + 1), serial)
     for i, c in enumerate(cases):
         assert np.array_equal(status[i], exp_status[i]), (c, status[i], exp_status[i])
     assert n == exp_table.shape[0]
@@ -187,10 +184,9 @@ def test_parallel_walk_8mib_vs_oracle(ramcrc, oracle_mod, value_len):
     certs[2, 1] ^= 0x10
     exp_status, exp_table, exp_crc = segment_cases.oracle_walk(oracle_mod, buf, certs, nseg, cap=cap)
     got = {}
-    for serial, shift, ordered in ((False, 0, False), (False, 13, False), (True, 0, False),
-                                   (False, 0, True)):
+    for serial, shift in ((False, 0), (False, 13), (True, 0)):
         status, n, table, crc = _run(ramcrc, buf, certs, nseg, cap, int(counts.sum()) * 2 + 1024,
-                                     serial, shift, ordered)
+                                     serial, shift)
         assert np.array_equal(status, exp_status), (serial, status, exp_status)
         assert n == exp_table.shape[0]
         t_dev, c_dev = _sorted(table, crc)

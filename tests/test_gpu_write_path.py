@@ -47,9 +47,8 @@ def _headers(buf, offs):
     return buf[idx].reshape(-1, 4).copy().view("<u4")[:, 0]
 
 
-@pytest.mark.parametrize("ordered", [False, True], ids=["any_order", "log_order"])
 @pytest.mark.parametrize("with_out", [True, False])
-def test_assemble_device_edge_lengths(ctx, oracle_mod, with_out, ordered):
+def test_assemble_device_edge_lengths(ctx, oracle_mod, with_out):
     rng = np.random.default_rng(8)
     lens = LENS + [int(x) for x in rng.integers(0, 9000, 400)]
     host, offs, lens = _packed(oracle_mod, lens, 31)
@@ -58,7 +57,7 @@ def test_assemble_device_edge_lengths(ctx, oracle_mod, with_out, ordered):
     off_t = torch.from_numpy(offs.view(np.int64)).cuda()
     len_t = torch.from_numpy(lens.view(np.int64)).cuda()
     out = torch.full((lens.size,), -1, dtype=torch.int32, device="cuda") if with_out else None
-    ctx.assemble_objects(d, off_t, len_t, out, ordered=ordered)
+    ctx.assemble_objects(d, off_t, len_t, out)
     torch.cuda.synchronize()
     ctx.check()
     got = d.cpu().numpy()
@@ -89,8 +88,7 @@ def test_assemble_then_verify_roundtrip(ctx, oracle_mod):
         assert oracle_mod.crc32c(buf[o + 4:o + L]) == stored
 
 
-@pytest.mark.parametrize("ordered", [False, True], ids=["any_order", "log_order"])
-def test_assemble_reference_goldens(ctx, golden, oracle_mod, ordered):
+def test_assemble_reference_goldens(ctx, golden, oracle_mod):
     objs = golden["object_checksums"]
     blobs = [b"\0\0\0\0" + bytes.fromhex(g["bytes"]) for g in objs]
     host = np.frombuffer(b"".join(blobs), np.uint8).copy()
@@ -98,25 +96,9 @@ def test_assemble_reference_goldens(ctx, golden, oracle_mod, ordered):
     lens = np.array([len(b) for b in blobs], np.uint64)
     d = torch.from_numpy(host).cuda()
     ctx.assemble_objects(d, torch.from_numpy(offs.view(np.int64)).cuda(),
-                         torch.from_numpy(lens.view(np.int64)).cuda(), ordered=ordered)
+                         torch.from_numpy(lens.view(np.int64)).cuda())
     torch.cuda.synchronize()
     assert list(_headers(d.cpu().numpy(), offs)) == [g["checksum"] for g in objs]
-
-
-def test_assemble_ordered_refused(ctx, ramcrc, oracle_mod):
-    """Overlapping objects in an ordered batch: nothing stamped, EORDER."""
-    host, offs, lens = _packed(oracle_mod, [100, 200, 300, 400], 77)
-    offs[2] = offs[1] + np.uint64(50)   # overlaps object 1
-    d = torch.from_numpy(host.copy()).cuda()
-    out = torch.full((4,), 7, dtype=torch.int32, device="cuda")
-    ctx.assemble_objects(d, torch.from_numpy(offs.view(np.int64)).cuda(),
-                         torch.from_numpy(lens.view(np.int64)).cuda(), out, ordered=True)
-    torch.cuda.synchronize()
-    assert np.array_equal(d.cpu().numpy(), host)
-    assert (out.cpu().numpy() == 7).all()
-    with pytest.raises(ramcrc.RamcrcError) as e:
-        ctx.check()
-    assert e.value.code == ramcrc.EORDER
 
 
 def test_assemble_host(ctx, oracle_mod):
