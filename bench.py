@@ -151,7 +151,7 @@ def roofline(kernel, algo_bytes, kernel_ms, traffic_key):
             "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
             "traffic": traffic, "traffic_source": src,
             "avg_kernel_ms": round(kernel_ms, 4),
-            "algorithmic_bytes_per_launch": algo_bytes}
+            "algorithmic_bytes_per_launch": algo_bytes, "traffic_key": traffic_key}
 
 
 # ------------------------------------------------------------ distributed
@@ -786,6 +786,7 @@ def run_replay(args, ranks):
     ctx.close()
     scan_s = scan_ms / args.steps / 1e3
     achieved = obj_bytes / scan_s / 1e9 if scan_s > 0 else None
+    tkey = f"replay_{nseg}x{args.seg_mib}MiB_v{args.value_len}_k_entries"
     return {
         "metric": "device-resident recovery replay verify GB/s of 8 MiB object segments "
                   "(segment walk + per-object checksum compare)",
@@ -807,10 +808,9 @@ def run_replay(args, ranks):
                      "achieved": round(achieved, 1) if achieved else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                     "traffic": traffic_for(f"replay_{nseg}x{args.seg_mib}MiB_v{args.value_len}_k_entries")[0],
-                     "traffic_source": traffic_for(
-                         f"replay_{nseg}x{args.seg_mib}MiB_v{args.value_len}_k_entries")[1],
-                     "scan_ms_per_step": round(scan_s * 1e3, 4)},
+                     "traffic": traffic_for(tkey)[0], "traffic_source": traffic_for(tkey)[1],
+                     "scan_ms_per_step": round(scan_s * 1e3, 4),
+                     "algorithmic_bytes_per_launch": obj_bytes, "traffic_key": tkey},
         "cpu_baseline": cpu,
         "all_segments_verified": ok,
     }

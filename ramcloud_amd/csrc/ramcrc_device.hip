@@ -204,6 +204,13 @@ constexpr uint32_t kHeadOff = kXinvOff + 1024;            // k_entries: head mas
 constexpr uint32_t kTailOff = kHeadOff + 21 * 32;         // k_entries: tail masks (272 B)
 constexpr uint32_t kBinOff = kTailOff + 17 * 16;          // k_entries: bin table (4 KiB)
 constexpr uint32_t kLdsEntries = kBinOff + 4096;          // 157616 B
+// the long phase's dynamic octet order (RAMCRC_LONG_DYN), after the bin table
+// (items 1296 B, starts 1288 B, costs 644 B) in the same 4 KiB
+constexpr uint32_t kDynPreOff = kBinOff + 3232;           // octets before each nonempty long bin (162 x 4 B)
+constexpr uint32_t kDynBinOff = kDynPreOff + 162 * 4;     // the nonempty long bins, descending (161 B)
+constexpr uint32_t kDynNneOff = kDynBinOff + 164;         // their number (4 B)
+constexpr uint32_t kDynExhOff = kDynNneOff + 4;           // workgroup: mask of drained claim counters
+static_assert(kDynExhOff + 4 <= kLdsEntries, "dynamic order fits the bin table's 4 KiB");
 static_assert(kBinOff % 16 == 0, "LDS table alignment");
 static_assert(kBinOff - kX4Off == sizeof(DeviceTables::LongTabs), "long-phase tables: LDS = g_tab.lt");
 static_assert(kLdsEntries <= 160 * 1024, "LDS budget");
@@ -957,6 +964,10 @@ constexpr uint64_t kOctetCost = RAMCRC_OCTET_COST;   // per-octet overhead in st
 // to skew 120-160 (config-3 mix +4 % over 80), replay verify (records mode)
 // loses from 120 on (-3 %), so records mode keeps 80.
 constexpr int kAgeSkew = RAMCRC_AGE_SKEW, kAgeSkewRec = RAMCRC_AGE_SKEW_REC;
+#ifndef RAMCRC_LONG_DYN
+#define RAMCRC_LONG_DYN 1   // long bins: octets claimed from 8 device counters (0: static shares)
+#endif
+constexpr int kClaimStride = 64;   // words between the long phase's claim counters (own 256 B lines)
 __host__ __device__ constexpr uint64_t age_weight(uint32_t r, int skew)
 {
     return uint64_t(2000 + skew * (3 - 2 * int(r)));
@@ -1045,6 +1056,7 @@ struct BinCounters {
     uint32_t pad_;
     uint32_t hs[kBinSlices][kNB];   // k_bin_one: histogram per slice of workgroups
     uint32_t arr[kBinSlices];       // k_bin_one: arrivals per slice
+    uint32_t claim[8 * kClaimStride];   // k_entries' long phase: octet claims, counter x at x * stride
 };
 
 constexpr uint32_t kBinGo = 1, kBinAbort = 2;   // BinCounters::flag: k_bin_one's vote
@@ -1165,6 +1177,8 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
             nx.hs[t / kNB][t % kNB] = 0;
         for (int t = threadIdx.x; t < kBinSlices; t += blockDim.x)
             nx.arr[t] = 0;
+        for (int t = threadIdx.x; t < 8; t += blockDim.x)
+            nx.claim[t * kClaimStride] = 0;
         if (threadIdx.x == 0) {
             nx.nlarge = 0;
             nx.ninact = 0;
@@ -1397,10 +1411,16 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter(BatchDesc d, Sorted so
     __shared__ uint64_t base[kNB];
     __shared__ BinScratch sc;
     __shared__ uint32_t tot[kNB];
+    __shared__ uint32_t vote;
     BinCounters& ctr = so.bt->ctr[so.par];
     if (rescue) {
-        if (ld_agent(&ctr.flag) == kBinGo)
-            return;   // (k_bin_one has ended: the flag is final and uniform)
+        // one load per workgroup (k_bin_one has ended: the flag is final); a
+        // load per thread put 250K same-address loads on the fabric (5 us)
+        if (threadIdx.x == 0)
+            vote = ld_agent(&ctr.flag);
+        __syncthreads();
+        if (vote == kBinGo)
+            return;
         for (int t = threadIdx.x; t < kNB; t += blockDim.x) {
             uint32_t all = 0;
 #pragma unroll
@@ -1588,6 +1608,8 @@ __global__ __launch_bounds__(kThreads) void k_bin_one(BatchDesc d, Sorted so, in
             nx.hs[t / kNB][t % kNB] = 0;
         for (int t = threadIdx.x; t < kBinSlices; t += blockDim.x)
             nx.arr[t] = 0;
+        for (int t = threadIdx.x; t < 8; t += blockDim.x)
+            nx.claim[t * kClaimStride] = 0;
         if (threadIdx.x == 0) {
             nx.nlarge = 0;
             nx.ninact = 0;
@@ -3065,6 +3087,85 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
     // 1-2 us per chunk; DESIGN.md section 5.4, profiles/r03/long.)
     if constexpr (kSmall) {
         run(I0 + T * wave / nwaves, I0 + T * (wave + 1) / nwaves);
+    } else if constexpr (RAMCRC_LONG_DYN != 0) {
+        // Dynamic order (round 5).  Static shares left the waves of the
+        // config-3 mix ending between 162 and 218 us (phase stamps,
+        // profiles/r05/stamps): inside a workgroup the SIMDs favour old waves
+        // by more than a fixed skew can match across workloads, and between
+        // workgroups the same work estimate ran 160-175 us depending on where
+        // in the bins it lay.  Here every wave claims one octet at a time,
+        // largest bins first (so the last claims are the shortest octets), from
+        // the 8 counters of the sequence: workgroup blk drains counter blk % 8
+        // (octets j = 8 k + x of the descending order, so each counter sees
+        // every bin), then the others.  A claim is issued one octet ahead and
+        // its descriptor fetched before the current octet runs, so neither
+        // latency is on the octet loop's path.
+        const uint32_t* dpre = reinterpret_cast<const uint32_t*>(lds + kDynPreOff);
+        const uint8_t* dbin = lds + kDynBinOff;
+        uint32_t* exh = reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(lds) + kDynExhOff);
+        const uint32_t nne = *reinterpret_cast<const uint32_t*>(lds + kDynNneOff);
+        const uint32_t ND = __builtin_amdgcn_readfirstlane(dpre[nne]);
+        uint32_t* claim = so.bt->ctr[so.par].claim;
+        uint32_t cx = blk & 7;
+        auto issue = [&]() -> uint32_t {
+            uint32_t t = 0;
+            if (lane == 0)
+                t = __hip_atomic_fetch_add(&claim[cx * kClaimStride], 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+            return t;
+        };
+        // the octet a ticket of counter cx stands for; ND when every counter is drained
+        auto resolve = [&](uint32_t t) -> uint32_t {
+            for (;;) {
+                const uint32_t j = 8 * __builtin_amdgcn_readfirstlane(t) + cx;
+                if (j < ND)
+                    return j;
+                uint32_t m = 0;
+                if (lane == 0)
+                    m = atomicOr(exh, 1u << cx);
+                m = __builtin_amdgcn_readfirstlane(m) | (1u << cx);
+                if (m == 0xFFu)
+                    return ND;
+                const uint32_t rot = ((~m & 0xFFu) >> cx) | ((~m & 0xFFu) << (8 - cx));
+                cx = (cx + __builtin_ctz(rot & 0xFFu)) & 7;
+                t = issue();
+            }
+        };
+        uint32_t mi = 0;   // nonempty bin of the last octet located
+        u32x4 nd = {0u, 0u, 0u, 0u};
+        uint32_t nix = kNoIdx, ninit = 0xFFFFFFFFu;
+        int nbin = 0;
+        auto fetch = [&](uint32_t j) {
+            if (j < dpre[mi])
+                mi = 0;
+            while (j >= dpre[mi + 1])
+                mi++;
+            mi = __builtin_amdgcn_readfirstlane(mi);
+            nbin = __builtin_amdgcn_readfirstlane(uint32_t(dbin[mi]));
+            const uint64_t sl = s_start[nbin] + uint64_t(j - dpre[mi]) * kG + g;
+            nd = so.desc[sl];
+            nix = so.idx[sl];
+            if (d.init)
+                ninit = so.init[sl];
+        };
+        uint32_t j = resolve(issue());
+        uint32_t t = 0;
+        if (j < ND) {
+            fetch(j);
+            t = issue();
+        }
+        while (j < ND) {
+            const u32x4 dd = nd;
+            const uint32_t ix = nix, init = ninit;
+            const int b = nbin;
+            const uint32_t jn = resolve(t);   // issued one octet ago
+            if (jn < ND) {
+                fetch(jn);   // the next octet's descriptor, before this octet runs
+                t = issue();
+            }
+            octet(dd, ix, init, b);
+            j = jn;
+        }
     } else {
         const uint64_t P0 = I0 + T * blk / nblk, PT = I0 + T * (blk + 1) / nblk - P0;
         const uint32_t slot = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
@@ -3196,6 +3297,45 @@ __global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc 
             s_cost[t] = uint32_t(so.bt->kcost[t]);
         }
     }
+#if RAMCRC_LONG_DYN
+    if (threadIdx.x < kWaveSize) {
+        // the long phase's octet order: nonempty long bins, largest first,
+        // with the octets before each (wave 0; the barrier below publishes it)
+        constexpr int kT = kTinyK > kSmallK ? kTinyK : kSmallK;
+        uint32_t* dpre = reinterpret_cast<uint32_t*>(lds + kDynPreOff);
+        uint8_t* dbin = lds + kDynBinOff;
+        const int lane = threadIdx.x;
+        uint32_t carry = 0, base = 0;
+        for (int c = 0; c * kWaveSize < kNB - (kT + 1); c++) {
+            const int b = kNB - 1 - c * kWaveSize - lane;
+            uint32_t oct = 0;
+            if (b > kT) {
+                const uint64_t it = so.bt->items[b + 1] - so.bt->items[b];
+                oct = it ? uint32_t(it / so.bt->kcost[b]) : 0u;
+            }
+            const uint64_t ne = __ballot(oct != 0);
+            uint32_t ps = oct;
+#pragma unroll
+            for (int sft = 1; sft < kWaveSize; sft <<= 1) {
+                const uint32_t a = __shfl_up(ps, sft, kWaveSize);
+                if (lane >= sft)
+                    ps += a;
+            }
+            const uint32_t rank = uint32_t(__popcll(ne & ((1ull << lane) - 1)));
+            if (oct) {
+                dbin[base + rank] = uint8_t(b);
+                dpre[base + rank] = carry + ps - oct;
+            }
+            carry += __shfl(ps, kWaveSize - 1, kWaveSize);
+            base += uint32_t(__popcll(ne));
+        }
+        if (lane == 0) {
+            dpre[base] = carry;
+            *reinterpret_cast<uint32_t*>(lds + kDynNneOff) = base;
+            *reinterpret_cast<uint32_t*>(lds + kDynExhOff) = 0u;
+        }
+    }
+#endif
     if (__syncthreads_or(bad)) {
         refuse();
         return;

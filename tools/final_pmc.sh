@@ -1,0 +1,20 @@
+# FETCH_SIZE passes (one counter pass per run, nothing else collected) of
+# every workload whose bench line reports roofline.traffic.  Afterwards, on
+# the build host:  python tools/final_pmc_digest.py OUT  -> profiles/pmc/*.json
+#     bash tools/final_pmc.sh [OUT]      (default gpurun_out/pmc)
+set -o pipefail
+OUT=gpurun_out/${1:-pmc}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+run() {   # name, bench arguments...
+  local n=$1; shift
+  timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/$n" -o p -- \
+      python3 bench.py "$@" --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/$n.json" 2> "$OUT/$n.err"
+}
+run c2 || exit 1
+run c4 --config recovery --no-t1 || exit 1
+run mix --config entries || exit 1
+run e100 --config entries --entry-size 100 || exit 1
+run append --config append || exit 1
+run replay --config replay || exit 1
+run replay64 --config replay --value-len 64 || exit 1

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--entry-size", type=int, default=0)
     ap.add_argument("--entries", type=int, default=1_000_000)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--save", default="", help="write the raw stamps (.npy)")
     a = ap.parse_args()
     import torch
     from ramcloud_amd import ramcrc, workloads
@@ -87,6 +88,14 @@ def main():
     if late.any():
         print(f"  workgroups whose tiny phase ended > 2 us after the median: {late.sum()}; their long-done mean "
               f"{e16.mean(1)[late].mean():.1f} vs {e16.mean(1)[~late].mean():.1f} for the others")
+    # long-phase duration per workgroup against its index: workgroups own
+    # contiguous ranges of the bins (small bins first), so a trend here is
+    # the work estimate (kcost) disagreeing with the time an octet takes
+    lg = (rel[:, 4] - rel[:, 2])[: len(end) // 16 * 16].reshape(-1, 16).mean(1)
+    dec = np.array_split(np.arange(lg.size), 8)
+    print("  long-phase mean by workgroup-index eighth:", " ".join(f"{lg[x].mean():.1f}" for x in dec))
+    if a.save:
+        np.save(a.save, raw)
     order = np.argsort(np.argsort(rel[:, 0].reshape(-1, 16), axis=1), axis=1).reshape(-1)
     print("  long-done median by start rank in workgroup:",
           " ".join(f"{np.median(end[order == x]):.1f}" for x in range(16)))
