@@ -266,6 +266,23 @@ int ramcrc_verify_objects_device(ramcrc_ctx* ctx, const void* d_base, uint64_t s
                                  const uint64_t* d_n_entries, uint32_t* d_obj_crc,
                                  ramcrc_seg_status* d_status, void* stream);
 
+/* The walk and the checks above in one call, as a recovery master replays a
+ * batch of segments right after walking them (RecoverySegmentBuilder::build
+ * then ObjectManager::replaySegment, src/RecoverySegmentBuilder.cc:61-203,
+ * src/ObjectManager.cc:585-1115): exactly ramcrc_segment_walk_device
+ * followed by ramcrc_verify_objects_device on the table it wrote (same
+ * arguments, same results, same record table), with one shortcut the split
+ * calls cannot take -- the walk notes whether any record it writes needs more
+ * than the one-window object path (a larger object, or a tombstone, safe
+ * version or transaction record), and when none does (RecoverSegmentBenchmark's
+ * small-value segments) the checks skip the binning pass over the table.
+ * Stream-ordered. */
+int ramcrc_replay_verify_device(ramcrc_ctx* ctx, const void* d_base, uint64_t seg_stride,
+                                uint32_t seg_capacity, uint64_t n_seg,
+                                const ramcrc_seg_cert* d_certs, ramcrc_seg_status* d_status,
+                                ramcrc_seg_entry* d_entries, uint64_t entries_cap,
+                                uint64_t* d_n_entries, uint32_t* d_obj_crc, void* stream);
+
 /* Host append path (src/Segment.cc:197-228 with src/Object.cc:213-218):
  * appends LOG_ENTRY_TYPE_OBJ entries holding objects {tableId 0, key = 8-byte
  * counter from first_key, version 0, timestamp 0, value_len value bytes} to an

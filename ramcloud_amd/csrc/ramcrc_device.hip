@@ -728,6 +728,23 @@ __device__ __forceinline__ bool replay_other(const u32x4& r)
     return hdr != 0 && !(type == RAMCRC_LOG_ENTRY_TYPE_OBJ && readable && !is_large(uint64_t(r.z) - 4));
 }
 
+// A walk record {segment, offset, length, header} the direct tiny path cannot
+// take by itself: a record k_obj_compare has work for, or an object whose
+// bytes [4, length) span more than one 128-byte window (the walk keeps
+// segments 16-byte aligned, so the window follows from the offset alone).
+// The fused replay call ORs this over every record its walk writes; when no
+// record is hard, the verify needs no binning (ramcrc_replay_verify_device).
+__device__ __forceinline__ bool replay_hard(uint32_t pos, uint32_t len, uint32_t hdr)
+{
+    const u32x4 r = {0u, pos, len, hdr};
+    if (replay_other(r))
+        return true;
+    if ((hdr & (0x3f | kRecOverlong)) != RAMCRC_LOG_ENTRY_TYPE_OBJ || len < kObjHeaderBytes)
+        return false;   // nothing to scan
+    const uint32_t s16 = (pos + 1 + ((hdr >> 6) & 3) + 1 + 4) & 15;   // S mod 16
+    return len - 4 >= 4 && s16 + (len - 4) > 128;
+}
+
 
 // Locate (entry, chunk) for global chunk index g in general mode.
 __device__ __forceinline__ void plan_locate(const Plan& pl, uint64_t n, uint64_t g, uint64_t& entry,
@@ -1160,8 +1177,14 @@ __device__ __forceinline__ uint32_t wave_bin_add(uint32_t* h, int b, bool active
 // bin's octet of padding slots only, whose interior loop bound Kmin - 1 then
 // wrapped: the k_entries hang of round 2.  Each log-scale bin's work estimate
 // now uses the bin's upper bound (bin_kmax).
+// sum (nullable; records mode, ramcrc_replay_verify_device): the walk's
+// replay_hard summary.  0: every record is inactive or a one-window object, so
+// the histogram is "all tiny" without reading the table -- the scatter then
+// publishes the direct path, which re-checks every record (a record that is
+// not tiny refuses the launch), and the plan and compare kernels find nothing.
 template <int kMode>
-__global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, int skip_large)
+__global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, int skip_large,
+                                                        const uint32_t* sum)
 {
     __shared__ uint32_t h[kNB];
     __shared__ uint32_t nlarge, ninact, nother;
@@ -1186,6 +1209,11 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
             nx.arrive = 0;
             nx.flag = 0;
         }
+    }
+    if (sum && *sum == 0) {
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            ctr.hist[1] = uint32_t(entry_count<kMode>(d));
+        return;
     }
     for (int t = threadIdx.x; t < kNB; t += blockDim.x)
         h[t] = 0;
@@ -3533,6 +3561,8 @@ struct ramcrc_ctx {
     uint64_t walk_blocks_cap = 0;
     unsigned long long* walk_pool_used = nullptr;
     uint64_t walk_pool_used_cap = 0;
+    uint32_t* walk_sum = nullptr;   // ramcrc_replay_verify_device: the walk's replay_hard summary
+    uint64_t walk_sum_cap = 0;
     bool serial_walk = false;   // RAMCRC_OPT_SERIAL_WALK
     uint32_t walk_pshift = 0;   // RAMCRC_OPT_WALK_PART_SHIFT; 0: kPartShift
     // benchmark timing of the scan kernels
@@ -3695,7 +3725,8 @@ uint64_t bin_grid(const ramcrc_ctx* c, uint64_t n)
 }
 
 template <int kMode>
-int bin_begin(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_large, Sorted* so)
+int bin_begin(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_large, Sorted* so,
+              const uint32_t* sum = nullptr)
 {
     if (d.n >= (1ull << 32))
         return RAMCRC_EINVAL;   // sorted slots keep 32-bit entry indices
@@ -3724,7 +3755,7 @@ int bin_begin(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_large, 
             nb = 0;
         resident = nb;
     }
-    if (RAMCRC_BIN_ONE && !c->dirty_bins && tiles > 0 &&
+    if (RAMCRC_BIN_ONE && !c->dirty_bins && !sum && tiles > 0 &&
         tiles <= uint64_t(c->ncu) * uint64_t(std::min(resident / 2, int(kBinWgsPerCu)))) {
         so->one = 1;
         hipLaunchKernelGGL(k_bin_one<kMode>, dim3(tiles), dim3(kThreads), 0, s, d, *so, skip_large,
@@ -3732,7 +3763,7 @@ int bin_begin(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_large, 
         c->bin_straggler = 0;
     } else {
         hipLaunchKernelGGL(k_bin_count<kMode>, dim3(bin_grid(c, d.n)), dim3(kThreads), 0, s, d,
-                           *so, skip_large);
+                           *so, skip_large, sum);
     }
     HIPCHK(hipGetLastError());
     // enqueued: it zeroes the other copy, which the next sequence uses
@@ -3778,10 +3809,11 @@ int launch_binned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_lar
 }
 
 template <int kMode>
-int launch_planned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, const uint32_t** nother = nullptr)
+int launch_planned(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, const uint32_t** nother = nullptr,
+                   const uint32_t* sum = nullptr)
 {
     Sorted so;
-    int rc = bin_begin<kMode>(c, d, s, 1, &so);
+    int rc = bin_begin<kMode>(c, d, s, 1, &so, sum);
     if (rc)
         return rc;
     if (nother)
@@ -3846,6 +3878,7 @@ struct WalkDesc {
     unsigned long long* n_entries;
     const uint32_t* only;   // nullable: walk only the segments with only[seg] != 0
     uint64_t* seg_base;     // nullable: per segment, the first slot of its records
+    uint32_t* sum;          // nullable: ORed with 1 when a written record is replay_hard
 };
 
 // CRC32C update by the m (1..4) bytes in the low end of v; t[j][b] = X^(j+1)(b).
@@ -3895,6 +3928,7 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
         xm[t] = g_tab.xmeta[t];
     __syncthreads();
     const int lane = threadIdx.x;
+    bool hard = false;   // a record this wave wrote is replay_hard (w.sum)
 
     for (uint64_t seg = blockIdx.x; seg < w.nseg; seg += gridDim.x) {
         if (w.only && !w.only[seg])
@@ -3950,8 +3984,10 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
                 rtotal += nrec;
             } else if (nrec) {
                 const unsigned long long b = rbase + rdone;
-                if (lane < int(nrec) && b + lane < w.cap)
+                if (lane < int(nrec) && b + lane < w.cap) {
                     w.entries[b + lane] = u32x4{uint32_t(seg), rpos, rlen, rinfo};
+                    hard = hard || (w.sum && replay_hard(rpos, rlen, rinfo));
+                }
                 rdone += nrec;
             }
             ns = 0;
@@ -4085,6 +4121,8 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
         }
         }   // pass
     }
+    if (w.sum && __ballot(hard) && lane == 0)
+        atomicOr(w.sum, 1u);
 }
 
 // ------------------------------------------------- parallel segment walk
@@ -4186,6 +4224,7 @@ struct PWalk {
     uint32_t* blocks;                // per part: kMaxBlocks pool block indices
     unsigned long long* pool_used;   // blocks taken (zeroed per launch)
     uint64_t pool_cap;               // pool blocks
+    uint32_t* sum;                   // nullable: as WalkDesc::sum
 };
 
 typedef const __attribute__((address_space(1))) uint32_t gu32;
@@ -4648,10 +4687,14 @@ struct TableSink {
     u32x4* out;
     uint64_t n;
     uint32_t seg;
+    bool* hard;   // nullable: set when a written record is replay_hard
     __device__ void operator()(uint32_t idx, uint32_t pos, uint32_t len, uint32_t hdr) const
     {
-        if (idx < n)
+        if (idx < n) {
             out[idx] = u32x4{seg, pos, len, hdr};
+            if (hard && replay_hard(pos, len, hdr))
+                *hard = true;
+        }
     }
 };
 
@@ -5294,6 +5337,7 @@ __global__ __launch_bounds__(256) void k_walk_emit(PWalk w0)
     }
     const bool chase = emit && (r.flags & (kPartChase | kPartSpill));
     const uint32_t pre = emit && !chase ? r.pre : 0u;
+    bool hard = false;
     if (chase || pre) {
         const uint32_t k = uint32_t(i - seg * w.nparts);
         const uint32_t B = k << w.pshift;
@@ -5303,9 +5347,12 @@ __global__ __launch_bounds__(256) void k_walk_emit(PWalk w0)
         const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
         PartRes x;
         walk_lane(w, tab, seg, sb, r.start, pend < limit ? pend : limit, x,
-                  TableSink{w.entries + slot, slot < w.cap ? w.cap - slot : 0, uint32_t(seg)},
+                  TableSink{w.entries + slot, slot < w.cap ? w.cap - slot : 0, uint32_t(seg),
+                            w.sum ? &hard : nullptr},
                   chase ? (1u << w.pshift) : pre);
     }
+    if (w.sum && __ballot(hard) && (threadIdx.x & (kWaveSize - 1)) == 0)
+        atomicOr(w.sum, 1u);
 }
 
 // C': the scratch records of the parts accepted without a second walk.  One
@@ -5327,6 +5374,7 @@ __global__ __launch_bounds__(256) void k_walk_copy(PWalk w0)
     const uint64_t nblk = nfirst + (used < w.pool_cap ? used : w.pool_cap);
     const uint64_t nwave = uint64_t(gridDim.x) * (blockDim.x / kWaveSize);
     const uint32_t lane = threadIdx.x & (kWaveSize - 1);
+    bool hard = false;
     for (uint64_t b0 = (uint64_t(blockIdx.x) * (blockDim.x / kWaveSize) +
                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize)) * kCopyU;
          b0 < nblk; b0 += nwave * kCopyU) {
@@ -5378,10 +5426,14 @@ __global__ __launch_bounds__(256) void k_walk_copy(PWalk w0)
             if (ri < r[u].cut || ri - r[u].cut >= n)
                 continue;
             const uint64_t dst = sbase[u] + r[u].rec + r[u].pre + (ri - r[u].cut);
-            if (dst < w.cap)
+            if (dst < w.cap) {
                 w.entries[dst] = u32x4{uint32_t(part[u] / w.nparts), v[u].x, v[u].y >> 8, v[u].y & 0xFF};
+                hard = hard || (w.sum && replay_hard(v[u].x, v[u].y >> 8, v[u].y & 0xFF));
+            }
         }
     }
+    if (w.sum && __ballot(hard) && lane == 0)
+        atomicOr(w.sum, 1u);
 }
 
 // ObjectManager::replaySegment's checksum checks on the walk records of the
@@ -5682,6 +5734,7 @@ int ramcrc_ctx_destroy(ramcrc_ctx* c)
     if (c->walk_pool_owner) (void)hipFree(c->walk_pool_owner);
     if (c->walk_blocks) (void)hipFree(c->walk_blocks);
     if (c->walk_pool_used) (void)hipFree(c->walk_pool_used);
+    if (c->walk_sum) (void)hipFree(c->walk_sum);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -6112,22 +6165,68 @@ int ramcrc_stream_host(ramcrc_ctx* c, const void* h_base, uint64_t seg_bytes, ui
 }
 
 
+namespace {
+int walk_impl(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride, uint32_t seg_capacity,
+              uint64_t n_seg, const ramcrc_seg_cert* d_certs, ramcrc_seg_status* d_status,
+              ramcrc_seg_entry* d_entries, uint64_t entries_cap, uint64_t* d_n_entries,
+              hipStream_t s, uint32_t* sum);
+int verify_impl(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride,
+                const ramcrc_seg_entry* d_entries, uint64_t entries_cap, const uint64_t* d_n_entries,
+                uint32_t* d_obj_crc, ramcrc_seg_status* d_status, hipStream_t s, const uint32_t* sum);
+}  // namespace
+
 int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride,
                                uint32_t seg_capacity, uint64_t n_seg,
                                const ramcrc_seg_cert* d_certs, ramcrc_seg_status* d_status,
                                ramcrc_seg_entry* d_entries, uint64_t entries_cap,
                                uint64_t* d_n_entries, void* stream)
 {
-    if (!c || !d_n_entries || (entries_cap && !d_entries))
+    if (!c)
+        return RAMCRC_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    return walk_impl(c, d_base, seg_stride, seg_capacity, n_seg, d_certs, d_status, d_entries,
+                     entries_cap, d_n_entries, reinterpret_cast<hipStream_t>(stream), nullptr);
+}
+
+int ramcrc_replay_verify_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride,
+                                uint32_t seg_capacity, uint64_t n_seg, const ramcrc_seg_cert* d_certs,
+                                ramcrc_seg_status* d_status, ramcrc_seg_entry* d_entries,
+                                uint64_t entries_cap, uint64_t* d_n_entries, uint32_t* d_obj_crc,
+                                void* stream)
+{
+    if (!c)
+        return RAMCRC_EINVAL;
+    if (entries_cap && !d_obj_crc)
+        return RAMCRC_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int rc = grow_device(reinterpret_cast<void**>(&c->walk_sum), &c->walk_sum_cap, 4, sizeof(uint32_t));
+    if (rc)
+        return rc;
+    HIPCHK(hipMemsetAsync(c->walk_sum, 0, sizeof(uint32_t), s));
+    rc = walk_impl(c, d_base, seg_stride, seg_capacity, n_seg, d_certs, d_status, d_entries,
+                   entries_cap, d_n_entries, s, c->walk_sum);
+    if (rc || n_seg == 0)
+        return rc;
+    return verify_impl(c, d_base, seg_stride, d_entries, entries_cap, d_n_entries, d_obj_crc,
+                       d_status, s, c->walk_sum);
+}
+
+namespace {
+int walk_impl(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride, uint32_t seg_capacity,
+              uint64_t n_seg, const ramcrc_seg_cert* d_certs, ramcrc_seg_status* d_status,
+              ramcrc_seg_entry* d_entries, uint64_t entries_cap, uint64_t* d_n_entries,
+              hipStream_t s, uint32_t* sum)
+{
+    if (!d_n_entries || (entries_cap && !d_entries))
         return RAMCRC_EINVAL;
     if (n_seg && (!d_base || !d_certs || !d_status))
         return RAMCRC_EINVAL;
     if ((reinterpret_cast<uintptr_t>(d_base) & 15) || (seg_stride & 15) || (seg_capacity & 15) ||
         n_seg > 0xFFFFFFFFull || (n_seg > 1 && seg_stride < seg_capacity))
         return RAMCRC_EINVAL;
-    std::lock_guard<std::recursive_mutex> lk(c->mu);
-    DeviceGuard g(c->device);
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     HIPCHK(hipMemsetAsync(d_n_entries, 0, sizeof(uint64_t), s));
     if (n_seg == 0)
         return RAMCRC_OK;
@@ -6142,6 +6241,7 @@ int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_s
     w.cap = entries_cap;
     w.n_entries = reinterpret_cast<unsigned long long*>(d_n_entries);
     w.only = nullptr;
+    w.sum = sum;
     {
         int rc0 = grow_device(reinterpret_cast<void**>(&c->walk_base), &c->walk_base_cap, n_seg,
                               sizeof(uint64_t));
@@ -6210,6 +6310,7 @@ int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_s
         pw.blocks = c->walk_blocks;
         pw.pool_used = c->walk_pool_used;
         pw.pool_cap = pool_blocks;
+        pw.sum = sum;
         HIPCHK(hipMemsetAsync(c->walk_pool_used, 0, sizeof(unsigned long long), s));
         hipLaunchKernelGGL(k_walk_probe, dim3(1), dim3(kWaveSize), 0, s, pw, c->walk_pshift, geo);
         HIPCHK(hipGetLastError());
@@ -6237,6 +6338,7 @@ int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_s
     HIPCHK(hipGetLastError());
     return RAMCRC_OK;
 }
+}  // namespace
 
 int ramcrc_segments_certify_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride,
                                    uint32_t seg_capacity, uint64_t n_seg, const uint32_t* d_heads,
@@ -6279,13 +6381,21 @@ int ramcrc_verify_objects_device(ramcrc_ctx* c, const void* d_base, uint64_t seg
 {
     if (!c)
         return RAMCRC_EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    return verify_impl(c, d_base, seg_stride, d_entries, entries_cap, d_n_entries, d_obj_crc,
+                       d_status, reinterpret_cast<hipStream_t>(stream), nullptr);
+}
+
+namespace {
+int verify_impl(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride,
+                const ramcrc_seg_entry* d_entries, uint64_t entries_cap, const uint64_t* d_n_entries,
+                uint32_t* d_obj_crc, ramcrc_seg_status* d_status, hipStream_t s, const uint32_t* sum)
+{
     if (entries_cap == 0)
         return RAMCRC_OK;
     if (!d_base || !d_entries || !d_n_entries || !d_obj_crc || !d_status)
         return RAMCRC_EINVAL;
-    std::lock_guard<std::recursive_mutex> lk(c->mu);
-    DeviceGuard g(c->device);
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int rc = reserve_locked(c, default_chunk_bound(entries_cap), entries_cap);
     if (rc)
         return rc;
@@ -6303,7 +6413,7 @@ int ramcrc_verify_objects_device(ramcrc_ctx* c, const void* d_base, uint64_t seg
     d.out = d_obj_crc;
     d.flags = RAMCRC_FINALIZE;
     const uint32_t* nother = nullptr;
-    rc = launch_planned<kRecords>(c, d, s, &nother);
+    rc = launch_planned<kRecords>(c, d, s, &nother, sum);
     if (rc)
         return rc;
     uint64_t grid = (entries_cap + 255) / 256;
@@ -6312,6 +6422,7 @@ int ramcrc_verify_objects_device(ramcrc_ctx* c, const void* d_base, uint64_t seg
     HIPCHK(hipGetLastError());
     return RAMCRC_OK;
 }
+}  // namespace
 
 int ramcrc_assemble_objects_device(ramcrc_ctx* c, void* d_base, const uint64_t* d_off,
                                    const uint64_t* d_len, uint32_t* d_out, uint64_t n,

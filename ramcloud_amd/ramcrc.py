@@ -80,6 +80,7 @@ def lib():
         "ramcrc_stream_host": (i32, [vp, vp, u64, u64, vp, u32, i32, i32]),
         "ramcrc_segment_walk_device": (i32, [vp, vp, u64, u32, u64, vp, vp, vp, u64, vp, vp]),
         "ramcrc_verify_objects_device": (i32, [vp, vp, u64, vp, u64, vp, vp, vp, vp]),
+        "ramcrc_replay_verify_device": (i32, [vp, vp, u64, u32, u64, vp, vp, vp, u64, vp, vp, vp]),
         "ramcrc_segments_certify_device": (i32, [vp, vp, u64, u32, u64, vp, vp, vp, vp]),
         "ramcrc_segment_fill_objects": (i32, [vp, u32, u32, u64, _c.POINTER(u32), vp]),
         "ramcrc_assemble_objects_device": (i32, [vp, vp, vp, vp, vp, u64, vp]),
@@ -372,6 +373,18 @@ class Context:
                                                 entries.shape[0], _ptr(n_entries), _ptr(obj_crc),
                                                 _ptr(status), _stream(stream))
         _check(rc, "ramcrc_verify_objects_device")
+        return status
+
+    def replay_verify(self, data, seg_stride, seg_capacity, nseg, certs, status, entries, n_entries,
+                      obj_crc, stream=None):
+        """segment_walk + verify_objects in one call (ramcrc_replay_verify_device):
+        same results; skips the binning pass when every record is a one-window
+        object."""
+        cap = 0 if entries is None else entries.shape[0]
+        rc = lib().ramcrc_replay_verify_device(self._h, _ptr(data), seg_stride, seg_capacity, nseg,
+                                               _ptr(certs), _ptr(status), _ptr(entries), cap,
+                                               _ptr(n_entries), _ptr(obj_crc), _stream(stream))
+        _check(rc, "ramcrc_replay_verify_device")
         return status
 
     def fill_objects(self, data, seg_stride, capacity, nseg, value_len, first_key=0, certs=None):

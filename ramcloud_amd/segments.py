@@ -152,7 +152,15 @@ class RecoveryVerify:
         reads the walked record count back (a host sync), and when the walk
         found more records than the table holds it is enlarged and the batch
         walked again, so that verify(check=False) never returns segments left
-        TABLE_FULL; fixed tables never sync unless check=True."""
+        TABLE_FULL; fixed tables never sync unless check=True, and take the
+        fused walk + verify call (ramcrc_replay_verify_device)."""
+        if not self.grow:
+            st = self.ctx.replay_verify(d_segments, self.stride, self.capacity, self.nseg, d_certs,
+                                        self.status, self.entries, self.n_entries, self.obj_crc,
+                                        stream=stream)
+            if check:
+                self.check(stream)
+            return st
         self.walk(d_segments, d_certs, stream)
         if self.grow:
             self.ctx.check(stream)

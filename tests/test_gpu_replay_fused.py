@@ -1,0 +1,100 @@
+"""ramcrc_replay_verify_device: the walk and the replay checks in one call.
+
+It must give exactly what ramcrc_segment_walk_device followed by
+ramcrc_verify_objects_device gives (status words, record table, object CRCs),
+on RecoverSegmentBenchmark-shaped segments
+(nanobenchmarks/RecoverSegmentBenchmark.cc:123-146) of 64-byte values -- where
+every record is a one-window object and the fused call skips the binning pass
+-- with one object's value damaged (bad_objects) and one certificate damaged
+(the whole segment fails, its records are inactive); and on a batch whose
+records are not all one-window objects (1 KiB values), where it takes the
+binned path.  Expected statuses come from the fill's certificate and the
+damage, independently of either device path."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+MiB = 1 << 20
+SEG = 8 * MiB
+
+
+def _batch(ramcrc, ctx, nseg, vlen, first_seed=0x5A17):
+    from ramcloud_amd import workloads
+    d = torch.empty(nseg * SEG, dtype=torch.uint8, device="cuda")
+    certs = torch.zeros((nseg, 2), dtype=torch.int32, device="cuda")
+    workloads.splitmix_fill_segments(d, SEG, first_seed)
+    per, length, ck = ctx.fill_objects(d, SEG, SEG, nseg, vlen, first_key=0, certs=certs)
+    torch.cuda.synchronize()
+    return d, certs, per, ck
+
+
+def _run(ramcrc, ctx, d, certs, nseg, cap, fused):
+    from ramcloud_amd import segments
+    rv = segments.RecoveryVerify(ctx, nseg, SEG, entries_cap=cap)
+    if fused:
+        st = rv.verify(d, certs, check=True)   # fixed table: the fused call
+    else:
+        rv.walk(d, certs)
+        st = rv.verify_objects(d)
+        rv.check()
+    torch.cuda.synchronize()
+    n = int(rv.n_entries.item())
+    return (st.cpu().numpy().view(np.uint32).copy(), n,
+            rv.entries[:n].cpu().numpy().view(np.uint32).copy(),
+            rv.obj_crc[:n].cpu().numpy().view(np.uint32).copy())
+
+
+def test_fused_equals_split_small_values(ramcrc):
+    from ramcloud_amd import segments
+    nseg, vlen = 16, 64
+    ctx = ramcrc.Context(0)
+    try:
+        d, certs, per, ck = _batch(ramcrc, ctx, nseg, vlen)
+        eb = segments.entry_bytes(vlen)
+        # segment 2: one byte of object 1000's value flipped (its checksum fails)
+        d[2 * SEG + 1000 * eb + eb - 3] ^= 0x40
+        # segment 5: a wrong certificate (the segment fails, its records are inactive)
+        certs[5, 1] ^= 0x100
+        cap = nseg * per + 1024
+        fs, fn, ft, fc = _run(ramcrc, ctx, d, certs, nseg, cap, fused=True)
+        # the shortcut was taken: the count pass put every record in bin 1
+        # (the binned path would have counted segment 5's records as inactive)
+        _, _, hist, par_next = ctx.debug_bins()
+        assert int(hist[par_next ^ 1][1]) == fn
+        ss, sn, st, sc = _run(ramcrc, ctx, d, certs, nseg, cap, fused=False)
+        assert fn == sn == nseg * per
+        assert np.array_equal(fs, ss)
+        assert np.array_equal(ft, st)
+        assert np.array_equal(fc, sc)
+        ok = np.ones(nseg, bool)
+        ok[5] = False
+        assert (fs[ok, 0] == segments.SEG_OK).all()
+        assert fs[5, 0] & segments.SEG_BAD_CHECKSUM and not fs[5, 0] & segments.SEG_OK
+        assert (fs[:, 2] == per).all()
+        bad = np.zeros(nseg, np.uint32)
+        bad[2] = 1
+        assert np.array_equal(fs[:, 3], bad)
+    finally:
+        ctx.close()
+
+
+def test_fused_equals_split_mixed_values(ramcrc):
+    """1 KiB values: records span several windows, so the fused call bins."""
+    from ramcloud_amd import segments
+    nseg, vlen = 8, 1024
+    ctx = ramcrc.Context(0)
+    try:
+        d, certs, per, ck = _batch(ramcrc, ctx, nseg, vlen, first_seed=0x77)
+        eb = segments.entry_bytes(vlen)
+        d[3 * SEG + 17 * eb + 100] ^= 1
+        cap = nseg * per + 1024
+        fs, fn, ft, fc = _run(ramcrc, ctx, d, certs, nseg, cap, fused=True)
+        ss, sn, st, sc = _run(ramcrc, ctx, d, certs, nseg, cap, fused=False)
+        assert fn == sn == nseg * per
+        assert np.array_equal(fs, ss) and np.array_equal(ft, st) and np.array_equal(fc, sc)
+        assert (fs[:, 0] == segments.SEG_OK).all()
+        assert list(fs[:, 3]) == [0, 0, 0, 1, 0, 0, 0, 0]
+    finally:
+        ctx.close()

@@ -5,7 +5,7 @@ O=gpurun_out/r05/longdyn
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
-    tests/test_gpu_parity.py tests/test_gpu_binning.py tests/test_gpu_segments.py tests/test_gpu_write_path.py \
+    tests/test_gpu_parity.py tests/test_gpu_binning.py tests/test_gpu_segments.py tests/test_gpu_write_path.py tests/test_gpu_replay_fused.py tests/test_gpu_segment_ref.py \
     > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
 L=ramcloud_amd/lib/variants/libramcrc_stamps.so
