@@ -141,12 +141,12 @@ class Crc32CBatch {
                        ramcrc_seg_entry* d_entries, uint64_t entriesCap, uint64_t* d_nEntries,
                        uint32_t* d_objCrc, void* stream = NULL)
     {
-        check(ramcrc_segment_walk_device(context(), d_base, stride, capacity, count, d_certs,
-                                         d_status, d_entries, entriesCap, d_nEntries, stream),
-              "ramcrc_segment_walk_device");
-        check(ramcrc_verify_objects_device(context(), d_base, stride, d_entries, entriesCap,
-                                           d_nEntries, d_objCrc, d_status, stream),
-              "ramcrc_verify_objects_device");
+        // walk + checks in one call (ramcrc_replay_verify_device): the same as
+        // ramcrc_segment_walk_device then ramcrc_verify_objects_device
+        check(ramcrc_replay_verify_device(context(), d_base, stride, capacity, count, d_certs,
+                                          d_status, d_entries, entriesCap, d_nEntries, d_objCrc,
+                                          stream),
+              "ramcrc_replay_verify_device");
         sync(stream);
     }
 
