@@ -96,6 +96,10 @@ struct alignas(16) DeviceTables {
     uint32_t xmeta[5 * 64 + 1];   // k_seg_walk: x^(8d), d = 0 .. 320 (one batch of metadata)
     uint32_t xbyte[4][256];       // x^(8 * b * 256^j): x^(8d) for any 32-bit d in 4 factors
     alignas(16) OpTable xinv128;  // tiny phase: X^-128 (a window sum moved back from the window end)
+    // Bases the tiny phase builds its LDS tables from (tiny_fill_gen):
+    // twb[q][k] = X^(128 - q)(1 << k), twib[j][k] = X^-128(1 << (8 j + k))
+    alignas(16) uint32_t twb[128][8];
+    alignas(16) uint32_t twib[4][8];
     // k_entries' long phase (group_fold, flush_batch, head and tail steps),
     // laid out as in LDS from kX4Off on, so one fill copies them all:
     struct alignas(16) LongTabs {
@@ -152,6 +156,14 @@ constexpr DeviceTables make_device_tables()
         for (int k = 0; k < 4; k++)
             for (uint32_t b = 0; b < 256; b++)
                 t.xinv128.t[k][b] = ramcrc::mulmod(b << (8 * k), c);
+        for (int k = 0; k < 4; k++)
+            for (int j = 0; j < 8; j++)
+                t.twib[k][j] = t.xinv128.t[k][1u << j];
+    }
+    for (int q = 0; q < 128; q++) {
+        const uint32_t c = ramcrc::xpow8(uint64_t(128 - q));
+        for (int j = 0; j < 8; j++)
+            t.twb[q][j] = ramcrc::mulmod(1u << j, c);
     }
     t.lt.x4 = t.comb[0];
     t.lt.x16 = t.comb[1];
@@ -2228,6 +2240,57 @@ __device__ __forceinline__ void tiny_fill_wr(uint8_t* lds)
 }
 #endif
 
+#ifndef RAMCRC_TINY_GEN
+#define RAMCRC_TINY_GEN 1   // tiny tables built in LDS from 8 basis words per row (0: copied from g_tab)
+#endif
+#if RAMCRC_TINY_GEN && !RAMCRC_TINY_LD16
+// The tiny phases' tables built in place instead of copied: X^m is linear, so
+// row q of X^(128 - q)(b) is the XOR of the basis words twb[q][k] over the set
+// bits k of b.  Thread t takes row q = t % 128 and the 32 columns b0 .. b0 + 31,
+// b0 = 32 (t / 128): T[b0] from bits 5-7, then T[b0 + i] = T[b0 + (i & (i - 1))]
+// ^ twb[q][ctz i] -- 31 XORs -- and 32 stores at immediate offsets (a wave's
+// 64 rows land on 32 banks).  Threads 0 .. 31 then build X^-128 the same way.
+// The copy it replaces moved 132 KiB per CU through the L2 (33 MB per launch
+// over the chip; 4.3 us of a 35 us 1M x 100 B launch, profiles/r04/ab).
+__device__ __forceinline__ void tiny_fill_gen(uint8_t* lds)
+{
+    static_assert(kEntWaves * kWaveSize == 1024, "one (row, column block) per thread");
+    const uint32_t q = threadIdx.x & 127, b0 = 32 * (threadIdx.x >> 7);
+    const uint4* bp = reinterpret_cast<const uint4*>(g_tab.twb[q]);
+    const uint4 lo = bp[0], hi = bp[1];
+    const uint32_t B[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    uint32_t iv[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    const bool inv = threadIdx.x < 32;   // X^-128: table j = t / 8, columns 32 (t % 8) ..
+    if (inv) {
+        const uint4* ip = reinterpret_cast<const uint4*>(g_tab.twib[threadIdx.x >> 3]);
+        const uint4 a = ip[0], c = ip[1];
+        iv[0] = a.x; iv[1] = a.y; iv[2] = a.z; iv[3] = a.w;
+        iv[4] = c.x; iv[5] = c.y; iv[6] = c.z; iv[7] = c.w;
+    }
+    uint32_t T[32];
+    T[0] = ((b0 >> 5) & 1 ? B[5] : 0u) ^ ((b0 >> 6) & 1 ? B[6] : 0u) ^ ((b0 >> 7) & 1 ? B[7] : 0u);
+#pragma unroll
+    for (int i = 1; i < 32; i++)
+        T[i] = T[i & (i - 1)] ^ B[__builtin_ctz(i)];
+    uint8_t* row = lds + (((q >> 6) << 16) | (b0 << 8) | ((q & 63) << 2));
+#pragma unroll
+    for (int i = 0; i < 32; i++)
+        *reinterpret_cast<uint32_t*>(row + 256 * i) = T[i];
+    if (inv) {
+        const uint32_t c0 = 32 * (threadIdx.x & 7);
+        uint32_t U[32];
+        U[0] = ((c0 >> 5) & 1 ? iv[5] : 0u) ^ ((c0 >> 6) & 1 ? iv[6] : 0u) ^ ((c0 >> 7) & 1 ? iv[7] : 0u);
+#pragma unroll
+        for (int i = 1; i < 32; i++)
+            U[i] = U[i & (i - 1)] ^ iv[__builtin_ctz(i)];
+        uint32_t* dst = reinterpret_cast<uint32_t*>(lds + kTwInvOff) + 256 * (threadIdx.x >> 3) + c0;
+#pragma unroll
+        for (int i = 0; i < 32; i++)
+            dst[i] = U[i];
+    }
+}
+#endif
+
 // Per-lane address constants: byte k of a rotated dword (window position
 // 32 j + 4 u + ((k + g4) & 3)) of dword pair j >> 1; + 128 for odd j.
 #if RAMCRC_TINY_LD16
@@ -2332,6 +2395,15 @@ __device__ __forceinline__ uint32_t tiny_win_wr(const uint8_t* lds, const u32x4&
 }
 #endif
 
+__device__ __forceinline__ void tiny_fill(uint8_t* lds)
+{
+#if RAMCRC_TINY_GEN && !RAMCRC_TINY_LD16
+    tiny_fill_gen(lds);
+#else
+    tiny_fill_wr(lds);
+#endif
+}
+
 // X^m(v) for 4 <= m <= 128 (byte k at distance m - k), and X^-128(v)
 __device__ __forceinline__ uint32_t tw_shift(const uint8_t* lds, uint32_t v, uint32_t m)
 {
@@ -2356,7 +2428,7 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
         // no entry of at most one window (uniform: every wave exits); the
         // multi-window phase still needs the table
         if (need_table) {
-            tiny_fill_wr(lds);
+            tiny_fill(lds);
             return !__syncthreads_or(bad);
         }
         return true;
@@ -2479,7 +2551,7 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
     issue(o0, wc, gc, sc);
 #endif
 #if RAMCRC_TINY_WR
-    tiny_fill_wr(lds);
+    tiny_fill(lds);
     const TwRows rw(gl, g4);
 #else
     fill_plain(lds, 0, g_tab.post, 256 * 128 + 128);
