@@ -1725,6 +1725,35 @@ __global__ __launch_bounds__(kThreads) void k_bin_one(BatchDesc d, Sorted so, in
     // (straggler: test hook, one workgroup more than launched, which never comes)
     if (!grid_arrive(ctr, gridDim.x + straggler))
         return;   // aborted: the guarded scatter bins the batch
+    constexpr bool kDirect = (kMode == kTable || kMode == kRecords) && RAMCRC_TINY_CF;
+    if constexpr (kDirect) {
+        // Every entry tiny (the direct path: nothing to scatter)?  Bins 0 and
+        // 1 and the inactive count decide it -- 17 loads instead of the 8 x 161
+        // below -- and then only workgroup 0 has work left: publishing the
+        // (empty) layout.
+        __shared__ uint32_t all_tiny;
+        if (threadIdx.x < 2) {
+            uint32_t all = 0;
+#pragma unroll
+            for (int j = 0; j < kBinSlices; j++)
+                all += ld_agent(&ctr.hs[j][threadIdx.x]);
+            h[threadIdx.x] = all;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+            all_tiny = uint64_t(h[0]) + h[1] + ld_agent(&ctr.ninact) == n;
+        __syncthreads();
+        if (all_tiny) {
+            if (blockIdx.x == 0) {
+                if (threadIdx.x < 2)
+                    ctr.hist[threadIdx.x] = h[threadIdx.x];
+                bin_layout(so, sc, true, n, h);   // direct: reads bins 0 and 1 only
+                for (int t = threadIdx.x; t < kNB; t += blockDim.x)
+                    ctr.cursor[t] = sc.count[t];
+            }
+            return;
+        }
+    }
     // totals, and this workgroup's place behind the earlier slices (reading
     // the slices here beat having the last arrival publish the totals)
     for (int t = threadIdx.x; t < kNB; t += blockDim.x) {
