@@ -1025,6 +1025,26 @@ constexpr int kBinSlices = RAMCRC_BIN_SLICES;
 #endif
 constexpr uint64_t kBinWgsPerCu = RAMCRC_BIN_WGS_PER_CU;   // binning grid cap per CU
 
+#ifndef RAMCRC_TINY_HM
+#define RAMCRC_TINY_HM 1   // 8-lane group XOR: third step by DPP row_half_mirror (0: ds_swizzle)
+#endif
+// XOR of the 8 lanes of a lane group (lanes 8g .. 8g + 7), in every lane:
+// quad permutes for lane ^ 1 and ^ 2; then every lane of a quad holds the
+// quad's XOR, and row_half_mirror (lane i of a half-row reads lane 7 - i)
+// brings in the other quad's -- a VALU op, where the ds_swizzle it replaces
+// was an LDS-pipe round trip per window.
+__device__ __forceinline__ uint32_t group8_xor_all(uint32_t R)
+{
+    R ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(R), 0xB1, 0xF, 0xF, false));   // lane ^ 1
+    R ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(R), 0x4E, 0xF, 0xF, false));   // lane ^ 2
+#if RAMCRC_TINY_HM
+    R ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(R), 0x141, 0xF, 0xF, false));  // row_half_mirror
+#else
+    R ^= uint32_t(__builtin_amdgcn_ds_swizzle(int(R), 0x1F | (4 << 10)));           // lane ^ 4
+#endif
+    return R;
+}
+
 constexpr uint32_t kTinyRow0 = 3;            // tiny phase: row of distance m is m + 3
 constexpr uint32_t kLdsTiny = 132 * 1024;    // tiny phase: X^m(byte), m = -3..128
 static_assert(kLdsTiny <= kLdsEntries, "k_entries' LDS holds the tiny phase's table");
@@ -2051,9 +2071,7 @@ __device__ __forceinline__ bool tiny_run(const BatchDesc& d, const Sorted& so, u
             const uint32_t t2 = xor3(v[6], v[7], v[8]), t3 = xor3(v[9], v[10], v[11]);
             const uint32_t t4 = xor3(v[12], v[13], v[14]);
             uint32_t R = xor3(xor3(t0, t1, t2), xor3(t3, t4, v[15]), 0u);
-            R ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(R), 0xB1, 0xF, 0xF, false));   // lane ^ 1
-            R ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(R), 0x4E, 0xF, 0xF, false));   // lane ^ 2
-            R ^= uint32_t(__builtin_amdgcn_ds_swizzle(int(R), 0x1F | (4 << 10)));           // lane ^ 4
+            R = group8_xor_all(R);
             mine = gl == q ? R : mine;
         }
         // own slot: the initial state (byte k at distance len - k), or bytewise
@@ -2384,9 +2402,7 @@ __device__ __forceinline__ uint32_t tiny_win_wr(const uint8_t* lds, const u32x4&
     const uint32_t a2 = xor3(v[6], v[7], v[8]), a3 = xor3(v[9], v[10], v[11]);
     const uint32_t a4 = xor3(v[12], v[13], v[14]);
     uint32_t R = xor3(xor3(a0, a1, a2), xor3(a3, a4, v[15]), 0u);
-    R ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(R), 0xB1, 0xF, 0xF, false));   // lane ^ 1
-    R ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(R), 0x4E, 0xF, 0xF, false));   // lane ^ 2
-    R ^= uint32_t(__builtin_amdgcn_ds_swizzle(int(R), 0x1F | (4 << 10)));           // lane ^ 4
+    R = group8_xor_all(R);
     return R;
 }
 #else
@@ -2417,9 +2433,7 @@ __device__ __forceinline__ uint32_t tiny_win_wr(const uint8_t* lds, const u32x4&
     const uint32_t t2 = xor3(v[6], v[7], v[8]), t3 = xor3(v[9], v[10], v[11]);
     const uint32_t t4 = xor3(v[12], v[13], v[14]);
     uint32_t R = xor3(xor3(t0, t1, t2), xor3(t3, t4, v[15]), 0u);
-    R ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(R), 0xB1, 0xF, 0xF, false));   // lane ^ 1
-    R ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(R), 0x4E, 0xF, 0xF, false));   // lane ^ 2
-    R ^= uint32_t(__builtin_amdgcn_ds_swizzle(int(R), 0x1F | (4 << 10)));           // lane ^ 4
+    R = group8_xor_all(R);
     return R;
 }
 #endif
@@ -2645,9 +2659,7 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
             const uint32_t t2 = xor3(v[6], v[7], v[8]), t3 = xor3(v[9], v[10], v[11]);
             const uint32_t t4 = xor3(v[12], v[13], v[14]);
             uint32_t R = xor3(xor3(t0, t1, t2), xor3(t3, t4, v[15]), 0u);
-            R ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(R), 0xB1, 0xF, 0xF, false));   // lane ^ 1
-            R ^= uint32_t(__builtin_amdgcn_update_dpp(0, int(R), 0x4E, 0xF, 0xF, false));   // lane ^ 2
-            R ^= uint32_t(__builtin_amdgcn_ds_swizzle(int(R), 0x1F | (4 << 10)));           // lane ^ 4
+            R = group8_xor_all(R);
             mine = gl == uint32_t(q) ? R : mine;
         }
 #endif

@@ -11,6 +11,6 @@ tail -2 $O/pytest.log
 L=ramcloud_amd/lib/variants/libramcrc_stamps.so
 RAMCRC_LIB=$L timeout -k 10 200 python tools/stamps.py --save $O/mix.npy > $O/stamps_mix.txt 2>&1 || exit 1
 cat $O/stamps_mix.txt
-VARIANTS="ld0 tg0" CASES="--config entries;--config entries --entry-size 100;--config entries --entry-size 1024;--config entries --entry-size 4096;--config append;--config replay;--config replay --value-len 64" \
+VARIANTS="ld0 tg0 hm0" CASES="--config entries;--config entries --entry-size 100;--config entries --entry-size 1024;--config entries --entry-size 4096;--config append;--config replay;--config replay --value-len 64" \
     REPS=3 STEPS=20 TAG=r05/longdyn/ab bash tools/gpu_ab.sh || exit 1
 python tools/ab_summary.py gpurun_out/r05/longdyn/ab
