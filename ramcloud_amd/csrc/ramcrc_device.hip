@@ -4756,6 +4756,68 @@ __device__ __forceinline__ void walk_lane(const PWalk& w, const uint32_t* tab, u
     walk_lane(w, tab, pos, stop, r, sink, budget, GlobalPeek{sb, w.capacity});
 }
 
+// A's walk with the entry after next loaded one hop early.  A part lane's
+// hops are a chain of memory round trips with one load in flight: dense parts
+// (64-byte values: ~650 entries per 64 KiB part, a new 128-byte line almost
+// every hop) took ~1.5 us a hop, 1 ms per 512 x 8 MiB batch.  Log entries of
+// one batch are mostly of one size (RecoverSegmentBenchmark's are exactly),
+// so the header after next is predicted at next + (next - pos) and loaded
+// while this hop's load is consumed: two lines in flight per lane.  A wrong
+// prediction costs the wasted load; the walk itself only ever uses the loads
+// of the offsets it actually reaches (results are unchanged).
+#ifndef RAMCRC_WALK_PRED
+#define RAMCRC_WALK_PRED 1
+#endif
+template <class Sink>
+__device__ __forceinline__ void walk_lane_pred(const PWalk& w, const uint32_t* tab, uint64_t sb,
+                                               uint32_t pos, uint32_t stop, PartRes& r, Sink&& sink,
+                                               uint32_t budget)
+{
+    const GlobalPeek peek{sb, w.capacity};
+    uint32_t count = 0, nmeta = 0, raw = 0, flags = kPartWalked, hops = 0;
+    uint64_t q = pos < stop ? peek(pos) : 0ull;
+    uint32_t ppos = kNoStart;   // predicted offset whose bytes pq holds
+    uint64_t pq = 0;
+    while (pos < stop) {
+        if (hops++ >= budget) {
+            flags |= kPartWrap;   // out of budget: the serial walker takes the segment
+            break;
+        }
+        const Hop h = hop_of(q, pos);
+        if (h.next > 0xFFFFFFFFull) {
+            flags |= kPartWrap;
+            nmeta += h.mbytes;
+            raw = meta_update(tab, raw, q, h.mbytes);
+            break;
+        }
+        if (h.next > w.capacity) {
+            flags |= kPartOverrun;
+            nmeta += h.mbytes;
+            raw = meta_update(tab, raw, q, h.mbytes);
+            break;
+        }
+        const uint32_t next = uint32_t(h.next);
+        uint64_t qn = pq;
+        if (next != ppos)
+            qn = next < stop ? peek(next) : 0ull;   // no prediction, or a wrong one
+        const uint32_t np = next + (next - pos);
+        ppos = np > next && np < stop ? np : kNoStart;
+        if (ppos != kNoStart)
+            pq = peek(ppos);
+        raw = meta_update(tab, raw, q, h.mbytes);
+        nmeta += h.mbytes;
+        sink(count, pos, h.len, uint32_t(q) & 0xFF);
+        count++;
+        pos = next;
+        q = qn;
+    }
+    r.exit = pos;
+    r.count = count;
+    r.nmeta = nmeta;
+    r.raw = raw;
+    r.flags = flags;
+}
+
 // B's re-walks are wave-uniform (every lane chases the same chain), so the
 // wave stages the segment bytes around the chain in LDS, kFixWin at a time,
 // and each hop reads LDS instead of waiting a memory round trip.
@@ -4880,7 +4942,11 @@ __global__ __launch_bounds__(256) void k_walk_parts(PWalk w0)
             const uint32_t pend = uint32_t(uint64_t(B) + (1ull << w.pshift) < w.capacity
                                                ? uint64_t(B) + (1ull << w.pshift) : w.capacity);
             const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
+#if RAMCRC_WALK_PRED
+            walk_lane_pred(w, tab, sb, start, pend < limit ? pend : limit, r,
+#else
             walk_lane(w, tab, seg, sb, start, pend < limit ? pend : limit, r,
+#endif
                       [&](uint32_t idx, uint32_t pos, uint32_t len, uint32_t hdr) {
                           // a part of at most kPartRec records keeps them in LDS
                           // for the wave's coalesced flush below; a denser part
