@@ -219,10 +219,10 @@ constexpr uint32_t kLdsEntries = kBinOff + 4096;          // 157616 B
 // the long phase's dynamic octet order (RAMCRC_LONG_DYN), after the bin table
 // (items 1296 B, starts 1288 B, costs 644 B) in the same 4 KiB
 constexpr uint32_t kDynPreOff = kBinOff + 3232;           // octets before each nonempty long bin (162 x 4 B)
-constexpr uint32_t kDynBinOff = kDynPreOff + 162 * 4;     // the nonempty long bins, descending (161 B)
+constexpr uint32_t kDynBinOff = kDynPreOff + 162 * 4;     // the nonempty long bins, ascending (161 B)
 constexpr uint32_t kDynNneOff = kDynBinOff + 164;         // their number (4 B)
-constexpr uint32_t kDynExhOff = kDynNneOff + 4;           // workgroup: mask of drained claim counters
-static_assert(kDynExhOff + 4 <= kLdsEntries, "dynamic order fits the bin table's 4 KiB");
+constexpr uint32_t kDynVicOff = kDynNneOff + 4;           // workgroup: next steal victim (4 B)
+static_assert(kDynVicOff + 4 <= kLdsEntries, "dynamic order fits the bin table's 4 KiB");
 static_assert(kBinOff % 16 == 0, "LDS table alignment");
 static_assert(kBinOff - kX4Off == sizeof(DeviceTables::LongTabs), "long-phase tables: LDS = g_tab.lt");
 static_assert(kLdsEntries <= 160 * 1024, "LDS budget");
@@ -994,9 +994,12 @@ constexpr uint64_t kOctetCost = RAMCRC_OCTET_COST;   // per-octet overhead in st
 // loses from 120 on (-3 %), so records mode keeps 80.
 constexpr int kAgeSkew = RAMCRC_AGE_SKEW, kAgeSkewRec = RAMCRC_AGE_SKEW_REC;
 #ifndef RAMCRC_LONG_DYN
-#define RAMCRC_LONG_DYN 1   // long bins: octets claimed from 8 device counters (0: static shares)
+#define RAMCRC_LONG_DYN 1   // long bins: per-workgroup octet deques with stealing (0: static shares)
 #endif
-constexpr int kClaimStride = 64;   // words between the long phase's claim counters (own 256 B lines)
+constexpr int kMaxDeq = 256;       // k_entries workgroups the deques cover (one per CU)
+#ifndef RAMCRC_STEAL_PROBES
+#define RAMCRC_STEAL_PROBES 8   // victims a workgroup tries once its own deque is empty
+#endif
 __host__ __device__ constexpr uint64_t age_weight(uint32_t r, int skew)
 {
     return uint64_t(2000 + skew * (3 - 2 * int(r)));
@@ -1012,6 +1015,9 @@ constexpr int kBinPer = RAMCRC_BIN_PER;    // entries per thread per tile (count
 #ifndef RAMCRC_BIN_RESCUE
 #define RAMCRC_BIN_RESCUE 1   // the guarded scatter after every k_bin_one (A/B only: 0 = none,
                               // an aborted k_bin_one then leaves its batch unbinned)
+#endif
+#ifndef RAMCRC_RESCUE_WGS
+#define RAMCRC_RESCUE_WGS 32   // guarded scatter's grid cap (0: one workgroup per tile)
 #endif
 #ifndef RAMCRC_BIN_SLICES
 #define RAMCRC_BIN_SLICES 8   // k_bin_one: histogram copies (workgroup i adds to copy i % 8: its XCD's)
@@ -1105,7 +1111,7 @@ struct BinCounters {
     uint32_t pad_;
     uint32_t hs[kBinSlices][kNB];   // k_bin_one: histogram per slice of workgroups
     uint32_t arr[kBinSlices];       // k_bin_one: arrivals per slice
-    uint32_t claim[8 * kClaimStride];   // k_entries' long phase: octet claims, counter x at x * stride
+    unsigned long long deq[kMaxDeq];   // k_entries' long phase: per workgroup, back << 32 | front
 };
 
 constexpr uint32_t kBinGo = 1, kBinAbort = 2;   // BinCounters::flag: k_bin_one's vote
@@ -1232,8 +1238,8 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
             nx.hs[t / kNB][t % kNB] = 0;
         for (int t = threadIdx.x; t < kBinSlices; t += blockDim.x)
             nx.arr[t] = 0;
-        for (int t = threadIdx.x; t < 8; t += blockDim.x)
-            nx.claim[t * kClaimStride] = 0;
+        for (int t = threadIdx.x; t < kMaxDeq; t += blockDim.x)
+            nx.deq[t] = 0;
         if (threadIdx.x == 0) {
             nx.nlarge = 0;
             nx.ninact = 0;
@@ -1668,8 +1674,8 @@ __global__ __launch_bounds__(kThreads) void k_bin_one(BatchDesc d, Sorted so, in
             nx.hs[t / kNB][t % kNB] = 0;
         for (int t = threadIdx.x; t < kBinSlices; t += blockDim.x)
             nx.arr[t] = 0;
-        for (int t = threadIdx.x; t < 8; t += blockDim.x)
-            nx.claim[t * kClaimStride] = 0;
+        for (int t = threadIdx.x; t < kMaxDeq; t += blockDim.x)
+            nx.deq[t] = 0;
         if (threadIdx.x == 0) {
             nx.nlarge = 0;
             nx.ninact = 0;
@@ -3228,48 +3234,80 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
     // 1-2 us per chunk; DESIGN.md section 5.4, profiles/r03/long.)
     if constexpr (kSmall) {
         run(I0 + T * wave / nwaves, I0 + T * (wave + 1) / nwaves);
-    } else if constexpr (RAMCRC_LONG_DYN != 0) {
-        // Dynamic order (round 5).  Static shares left the waves of the
-        // config-3 mix ending between 162 and 218 us (phase stamps,
+    } else if (RAMCRC_LONG_DYN != 0 && nblk <= uint32_t(kMaxDeq)) {
+        // Work-stealing deques (round 5).  Static shares left the waves of
+        // the config-3 mix ending between 160 and 218 us (phase stamps,
         // profiles/r05/stamps): inside a workgroup the SIMDs favour old waves
-        // by more than a fixed skew can match across workloads, and between
-        // workgroups the same work estimate ran 160-175 us depending on where
-        // in the bins it lay.  Here every wave claims one octet at a time,
-        // largest bins first (so the last claims are the shortest octets), from
-        // the 8 counters of the sequence: workgroup blk drains counter blk % 8
-        // (octets j = 8 k + x of the descending order, so each counter sees
-        // every bin), then the others.  A claim is issued one octet ahead and
-        // its descriptor fetched before the current octet runs, so neither
-        // latency is on the octet loop's path.
-        const uint32_t* dpre = reinterpret_cast<const uint32_t*>(lds + kDynPreOff);
-        const uint8_t* dbin = lds + kDynBinOff;
-        uint32_t* exh = reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(lds) + kDynExhOff);
+        // by more than a fixed skew matches, and between workgroups the same
+        // work estimate ran 160-175 us depending on where in the bins it lay.
+        // Workgroup blk owns the same contiguous range of octets its static
+        // share covered (octets numbered in bin order, a range = the octets
+        // whose first work unit lies in the share), as a deque in one 64-bit
+        // device word, back << 32 | front.  Its waves take octets from the
+        // front, one atomic add each, issued one octet ahead; a workgroup
+        // whose deque is empty steals single octets from the back of other
+        // workgroups' deques (subtracting 1 << 32).  Owner and thief never
+        // both get an octet: the atomic that moves front past back, or back to
+        // front, sees an empty range.  Octets stay in address order within a
+        // workgroup's range, which the interleaved form of this (8 counters
+        // over a global largest-first order) lost: it balanced the waves to
+        // 3 us but ran 1.2-1.5x slower (profiles/r05/longdyn/ab_long.txt).
+        constexpr uint32_t kNoOct = 0xFFFFFFFFu;
+        const uint32_t* opre = reinterpret_cast<const uint32_t*>(lds + kDynPreOff);
+        const uint8_t* obin = lds + kDynBinOff;
+        uint32_t* vic = reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(lds) + kDynVicOff);
         const uint32_t nne = *reinterpret_cast<const uint32_t*>(lds + kDynNneOff);
-        const uint32_t ND = __builtin_amdgcn_readfirstlane(dpre[nne]);
-        uint32_t* claim = so.bt->ctr[so.par].claim;
-        uint32_t cx = blk & 7;
-        auto issue = [&]() -> uint32_t {
-            uint32_t t = 0;
+        unsigned long long* deq = so.bt->ctr[so.par].deq;
+        // octets whose first work unit lies below item p
+        auto oct_at = [&](uint64_t p) -> uint32_t {
+            uint32_t m = 0;
+            while (m < nne && s_items[obin[m] + 1] <= p)
+                m++;
+            if (m == nne)
+                return opre[nne];
+            const int b = obin[m];
+            const uint64_t ib = s_items[b];
+            const uint32_t o = p > ib ? uint32_t((p - ib + s_cost[b] - 1) / s_cost[b]) : 0u;
+            return opre[m] + o;
+        };
+        auto range_of = [&](uint32_t k, uint32_t& lo, uint32_t& hi) {
+            lo = __builtin_amdgcn_readfirstlane(oct_at(I0 + T * k / nblk));
+            hi = __builtin_amdgcn_readfirstlane(oct_at(I0 + T * (k + 1) / nblk));
+        };
+        // the deque of this workgroup was initialised by its wave 0 before the
+        // phase's barrier (k_entries); a ticket is the old word of an atomic add
+        auto take = [&](uint32_t v, bool steal) -> unsigned long long {
+            unsigned long long t = 0;
             if (lane == 0)
-                t = __hip_atomic_fetch_add(&claim[cx * kClaimStride], 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
+                t = __hip_atomic_fetch_add(&deq[v], steal ? 0xFFFFFFFF00000000ull : 1ull,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return t;
         };
-        // the octet a ticket of counter cx stands for; ND when every counter is drained
-        auto resolve = [&](uint32_t t) -> uint32_t {
+        uint32_t victim = blk;   // whose deque the ticket is on
+        bool steal = false;
+        uint32_t vlo = 0, vhi = 0;   // the victim's range (a stolen octet must lie in it)
+        // the octet a ticket stands for; kNoOct when this workgroup is done
+        auto resolve = [&](unsigned long long t) -> uint32_t {
             for (;;) {
-                const uint32_t j = 8 * __builtin_amdgcn_readfirstlane(t) + cx;
-                if (j < ND)
-                    return j;
-                uint32_t m = 0;
+                const uint32_t f = __builtin_amdgcn_readfirstlane(uint32_t(t));
+                const uint32_t bk = __builtin_amdgcn_readfirstlane(uint32_t(t >> 32));
+                if (f < bk) {
+                    const uint32_t o = steal ? bk - 1 : f;
+                    if (!steal || (o >= vlo && o < vhi))   // (a deque not yet set up reads
+                        return o;                           // as a garbage range)
+                }
+                // this deque is empty: the next victim (shared by the workgroup's waves)
+                uint32_t k = 0;
                 if (lane == 0)
-                    m = atomicOr(exh, 1u << cx);
-                m = __builtin_amdgcn_readfirstlane(m) | (1u << cx);
-                if (m == 0xFFu)
-                    return ND;
-                const uint32_t rot = ((~m & 0xFFu) >> cx) | ((~m & 0xFFu) << (8 - cx));
-                cx = (cx + __builtin_ctz(rot & 0xFFu)) & 7;
-                t = issue();
+                    k = atomicAdd(vic, 1u);
+                k = __builtin_amdgcn_readfirstlane(k);
+                if (k >= uint32_t(RAMCRC_STEAL_PROBES) || k + 1 >= nblk)
+                    return kNoOct;
+                // victims spread over the grid: blk + 1, + 3, + 7, ...
+                victim = (blk + ((2u << k) - 1)) % nblk;
+                steal = true;
+                range_of(victim, vlo, vhi);
+                t = take(victim, true);
             }
         };
         uint32_t mi = 0;   // nonempty bin of the last octet located
@@ -3277,32 +3315,32 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
         uint32_t nix = kNoIdx, ninit = 0xFFFFFFFFu;
         int nbin = 0;
         auto fetch = [&](uint32_t j) {
-            if (j < dpre[mi])
+            if (j < opre[mi])
                 mi = 0;
-            while (j >= dpre[mi + 1])
+            while (j >= opre[mi + 1])
                 mi++;
             mi = __builtin_amdgcn_readfirstlane(mi);
-            nbin = __builtin_amdgcn_readfirstlane(uint32_t(dbin[mi]));
-            const uint64_t sl = s_start[nbin] + uint64_t(j - dpre[mi]) * kG + g;
+            nbin = __builtin_amdgcn_readfirstlane(uint32_t(obin[mi]));
+            const uint64_t sl = s_start[nbin] + uint64_t(j - opre[mi]) * kG + g;
             nd = so.desc[sl];
             nix = so.idx[sl];
             if (d.init)
                 ninit = so.init[sl];
         };
-        uint32_t j = resolve(issue());
-        uint32_t t = 0;
-        if (j < ND) {
+        uint32_t j = resolve(take(blk, false));
+        unsigned long long t = 0;
+        if (j != kNoOct) {
             fetch(j);
-            t = issue();
+            t = take(victim, steal);
         }
-        while (j < ND) {
+        while (j != kNoOct) {
             const u32x4 dd = nd;
             const uint32_t ix = nix, init = ninit;
             const int b = nbin;
             const uint32_t jn = resolve(t);   // issued one octet ago
-            if (jn < ND) {
+            if (jn != kNoOct) {
                 fetch(jn);   // the next octet's descriptor, before this octet runs
-                t = issue();
+                t = take(victim, steal);
             }
             octet(dd, ix, init, b);
             j = jn;
@@ -3439,18 +3477,19 @@ __global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc 
         }
     }
 #if RAMCRC_LONG_DYN
-    if (threadIdx.x < kWaveSize) {
-        // the long phase's octet order: nonempty long bins, largest first,
-        // with the octets before each (wave 0; the barrier below publishes it)
+    if (threadIdx.x < kWaveSize && gridDim.x <= kMaxDeq) {
+        // the long phase's octet numbering: nonempty long bins in ascending
+        // order with the octets before each; then this workgroup's deque
+        // (wave 0; the barrier below publishes both to the workgroup)
         constexpr int kT = kTinyK > kSmallK ? kTinyK : kSmallK;
-        uint32_t* dpre = reinterpret_cast<uint32_t*>(lds + kDynPreOff);
-        uint8_t* dbin = lds + kDynBinOff;
+        uint32_t* opre = reinterpret_cast<uint32_t*>(lds + kDynPreOff);
+        uint8_t* obin = lds + kDynBinOff;
         const int lane = threadIdx.x;
         uint32_t carry = 0, base = 0;
         for (int c = 0; c * kWaveSize < kNB - (kT + 1); c++) {
-            const int b = kNB - 1 - c * kWaveSize - lane;
+            const int b = kT + 1 + c * kWaveSize + lane;
             uint32_t oct = 0;
-            if (b > kT) {
+            if (b < kNB) {
                 const uint64_t it = so.bt->items[b + 1] - so.bt->items[b];
                 oct = it ? uint32_t(it / so.bt->kcost[b]) : 0u;
             }
@@ -3464,16 +3503,35 @@ __global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc 
             }
             const uint32_t rank = uint32_t(__popcll(ne & ((1ull << lane) - 1)));
             if (oct) {
-                dbin[base + rank] = uint8_t(b);
-                dpre[base + rank] = carry + ps - oct;
+                obin[base + rank] = uint8_t(b);
+                opre[base + rank] = carry + ps - oct;
             }
             carry += __shfl(ps, kWaveSize - 1, kWaveSize);
             base += uint32_t(__popcll(ne));
         }
         if (lane == 0) {
-            dpre[base] = carry;
+            opre[base] = carry;
             *reinterpret_cast<uint32_t*>(lds + kDynNneOff) = base;
-            *reinterpret_cast<uint32_t*>(lds + kDynExhOff) = 0u;
+            *reinterpret_cast<uint32_t*>(lds + kDynVicOff) = 0u;
+            // this workgroup's share, as the static split cuts the work units
+            // (the same arithmetic as the long phase's range_of)
+            const uint64_t I0 = so.bt->items[kT + 1], T = so.bt->items[kNB] - I0;
+            auto oct_at = [&](uint64_t p) -> uint32_t {
+                uint32_t m = 0;
+                while (m < base && so.bt->items[obin[m] + 1] <= p)
+                    m++;
+                if (m == base)
+                    return carry;
+                const int b = obin[m];
+                const uint64_t ib = so.bt->items[b], cost = so.bt->kcost[b];
+                return opre[m] + (p > ib ? uint32_t((p - ib + cost - 1) / cost) : 0u);
+            };
+            const uint32_t lo = oct_at(I0 + T * blockIdx.x / gridDim.x);
+            const uint32_t hi = oct_at(I0 + T * (blockIdx.x + 1) / gridDim.x);
+            __hip_atomic_store(&so.bt->ctr[so.par].deq[blockIdx.x],
+                               (static_cast<unsigned long long>(hi) << 32) | lo, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_s_waitcnt(0);
         }
     }
 #endif
@@ -3898,9 +3956,15 @@ int bin_finish(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_large,
         HIPCHK(hipGetLastError());
     }
     if (!so.one || RAMCRC_BIN_RESCUE) {
-        // after k_bin_one: the guarded scatter (exits at once unless k_bin_one aborted)
-        hipLaunchKernelGGL(k_bin_scatter<kMode>, dim3(bin_grid(c, d.n)), dim3(kThreads), 0, s, d,
-                           so, skip_large, int(so.one));
+        // after k_bin_one: the guarded scatter, which exits at once unless
+        // k_bin_one aborted -- on a smaller grid (grid-stride over the tiles),
+        // since every batch pays its dispatch and only an abort its work
+        uint64_t grid = bin_grid(c, d.n);
+        constexpr uint64_t kRescueWgs = RAMCRC_RESCUE_WGS;
+        if (so.one && kRescueWgs != 0 && grid > kRescueWgs)
+            grid = kRescueWgs;
+        hipLaunchKernelGGL(k_bin_scatter<kMode>, dim3(grid), dim3(kThreads), 0, s, d, so, skip_large,
+                           int(so.one));
         HIPCHK(hipGetLastError());
     }
     {
@@ -4756,68 +4820,6 @@ __device__ __forceinline__ void walk_lane(const PWalk& w, const uint32_t* tab, u
     walk_lane(w, tab, pos, stop, r, sink, budget, GlobalPeek{sb, w.capacity});
 }
 
-// A's walk with the entry after next loaded one hop early.  A part lane's
-// hops are a chain of memory round trips with one load in flight: dense parts
-// (64-byte values: ~650 entries per 64 KiB part, a new 128-byte line almost
-// every hop) took ~1.5 us a hop, 1 ms per 512 x 8 MiB batch.  Log entries of
-// one batch are mostly of one size (RecoverSegmentBenchmark's are exactly),
-// so the header after next is predicted at next + (next - pos) and loaded
-// while this hop's load is consumed: two lines in flight per lane.  A wrong
-// prediction costs the wasted load; the walk itself only ever uses the loads
-// of the offsets it actually reaches (results are unchanged).
-#ifndef RAMCRC_WALK_PRED
-#define RAMCRC_WALK_PRED 1
-#endif
-template <class Sink>
-__device__ __forceinline__ void walk_lane_pred(const PWalk& w, const uint32_t* tab, uint64_t sb,
-                                               uint32_t pos, uint32_t stop, PartRes& r, Sink&& sink,
-                                               uint32_t budget)
-{
-    const GlobalPeek peek{sb, w.capacity};
-    uint32_t count = 0, nmeta = 0, raw = 0, flags = kPartWalked, hops = 0;
-    uint64_t q = pos < stop ? peek(pos) : 0ull;
-    uint32_t ppos = kNoStart;   // predicted offset whose bytes pq holds
-    uint64_t pq = 0;
-    while (pos < stop) {
-        if (hops++ >= budget) {
-            flags |= kPartWrap;   // out of budget: the serial walker takes the segment
-            break;
-        }
-        const Hop h = hop_of(q, pos);
-        if (h.next > 0xFFFFFFFFull) {
-            flags |= kPartWrap;
-            nmeta += h.mbytes;
-            raw = meta_update(tab, raw, q, h.mbytes);
-            break;
-        }
-        if (h.next > w.capacity) {
-            flags |= kPartOverrun;
-            nmeta += h.mbytes;
-            raw = meta_update(tab, raw, q, h.mbytes);
-            break;
-        }
-        const uint32_t next = uint32_t(h.next);
-        uint64_t qn = pq;
-        if (next != ppos)
-            qn = next < stop ? peek(next) : 0ull;   // no prediction, or a wrong one
-        const uint32_t np = next + (next - pos);
-        ppos = np > next && np < stop ? np : kNoStart;
-        if (ppos != kNoStart)
-            pq = peek(ppos);
-        raw = meta_update(tab, raw, q, h.mbytes);
-        nmeta += h.mbytes;
-        sink(count, pos, h.len, uint32_t(q) & 0xFF);
-        count++;
-        pos = next;
-        q = qn;
-    }
-    r.exit = pos;
-    r.count = count;
-    r.nmeta = nmeta;
-    r.raw = raw;
-    r.flags = flags;
-}
-
 // B's re-walks are wave-uniform (every lane chases the same chain), so the
 // wave stages the segment bytes around the chain in LDS, kFixWin at a time,
 // and each hop reads LDS instead of waiting a memory round trip.
@@ -4942,11 +4944,7 @@ __global__ __launch_bounds__(256) void k_walk_parts(PWalk w0)
             const uint32_t pend = uint32_t(uint64_t(B) + (1ull << w.pshift) < w.capacity
                                                ? uint64_t(B) + (1ull << w.pshift) : w.capacity);
             const uint64_t sb = reinterpret_cast<uint64_t>(w.base) + seg * w.stride;
-#if RAMCRC_WALK_PRED
-            walk_lane_pred(w, tab, sb, start, pend < limit ? pend : limit, r,
-#else
             walk_lane(w, tab, seg, sb, start, pend < limit ? pend : limit, r,
-#endif
                       [&](uint32_t idx, uint32_t pos, uint32_t len, uint32_t hdr) {
                           // a part of at most kPartRec records keeps them in LDS
                           // for the wave's coalesced flush below; a denser part

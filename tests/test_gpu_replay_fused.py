@@ -41,9 +41,12 @@ def _run(ramcrc, ctx, d, certs, nseg, cap, fused):
         rv.check()
     torch.cuda.synchronize()
     n = int(rv.n_entries.item())
-    return (st.cpu().numpy().view(np.uint32).copy(), n,
-            rv.entries[:n].cpu().numpy().view(np.uint32).copy(),
-            rv.obj_crc[:n].cpu().numpy().view(np.uint32).copy())
+    table = rv.entries[:n].cpu().numpy().view(np.uint32)
+    crc = rv.obj_crc[:n].cpu().numpy().view(np.uint32)
+    # records come out in increasing order within a segment, in no fixed
+    # order across segments (include/ramcrc.h): compare by (segment, offset)
+    order = np.lexsort((table[:, 1], table[:, 0]))
+    return st.cpu().numpy().view(np.uint32).copy(), n, table[order], crc[order]
 
 
 def test_fused_equals_split_small_values(ramcrc):
