@@ -997,6 +997,7 @@ constexpr int kAgeSkew = RAMCRC_AGE_SKEW, kAgeSkewRec = RAMCRC_AGE_SKEW_REC;
 #define RAMCRC_LONG_DYN 1   // long bins: per-workgroup octet deques with stealing (0: static shares)
 #endif
 constexpr int kMaxDeq = 256;       // k_entries workgroups the deques cover (one per CU)
+constexpr uint32_t kDeqBias = 0x80000000u;   // both deque halves (see the long phase)
 #ifndef RAMCRC_STEAL_PROBES
 #define RAMCRC_STEAL_PROBES 8   // victims a workgroup tries once its own deque is empty
 #endif
@@ -3248,7 +3249,12 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
         // whose deque is empty steals single octets from the back of other
         // workgroups' deques (subtracting 1 << 32).  Owner and thief never
         // both get an octet: the atomic that moves front past back, or back to
-        // front, sees an empty range.  Octets stay in address order within a
+        // front, sees an empty range.  Both halves are biased by 2^31
+        // (kDeqBias), so the failing steals that keep decrementing an empty
+        // deque's back can never wrap it below its front (an unbiased back of
+        // 3 reached 0xFFFFFFFF after four of them, the empty deque looked full
+        // and its owner claimed octets past the table: an illegal address on
+        // the first GPU run of this form).  Octets stay in address order within a
         // workgroup's range, which the interleaved form of this (8 counters
         // over a global largest-first order) lost: it balanced the waves to
         // 3 us but ran 1.2-1.5x slower (profiles/r05/longdyn/ab_long.txt).
@@ -3286,15 +3292,18 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
         uint32_t victim = blk;   // whose deque the ticket is on
         bool steal = false;
         uint32_t vlo = 0, vhi = 0;   // the victim's range (a stolen octet must lie in it)
+        uint32_t own_lo, own_hi;
+        range_of(blk, own_lo, own_hi);
         // the octet a ticket stands for; kNoOct when this workgroup is done
         auto resolve = [&](unsigned long long t) -> uint32_t {
             for (;;) {
                 const uint32_t f = __builtin_amdgcn_readfirstlane(uint32_t(t));
                 const uint32_t bk = __builtin_amdgcn_readfirstlane(uint32_t(t >> 32));
                 if (f < bk) {
-                    const uint32_t o = steal ? bk - 1 : f;
-                    if (!steal || (o >= vlo && o < vhi))   // (a deque not yet set up reads
-                        return o;                           // as a garbage range)
+                    const uint32_t o = (steal ? bk - 1 : f) - kDeqBias;
+                    // (a victim's deque not yet set up holds no valid range)
+                    if (o >= (steal ? vlo : own_lo) && o < (steal ? vhi : own_hi))
+                        return o;
                 }
                 // this deque is empty: the next victim (shared by the workgroup's waves)
                 uint32_t k = 0;
@@ -3314,7 +3323,13 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
         u32x4 nd = {0u, 0u, 0u, 0u};
         uint32_t nix = kNoIdx, ninit = 0xFFFFFFFFu;
         int nbin = 0;
+        const uint32_t ND = opre[nne];
         auto fetch = [&](uint32_t j) {
+            if (j >= ND) {   // never (resolve validates every index); no load past the table
+                nd = u32x4{0u, 0u, 0u, 0u};
+                nix = kNoIdx;
+                return;
+            }
             if (j < opre[mi])
                 mi = 0;
             while (j >= opre[mi + 1])
@@ -3529,8 +3544,8 @@ __global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc 
             const uint32_t lo = oct_at(I0 + T * blockIdx.x / gridDim.x);
             const uint32_t hi = oct_at(I0 + T * (blockIdx.x + 1) / gridDim.x);
             __hip_atomic_store(&so.bt->ctr[so.par].deq[blockIdx.x],
-                               (static_cast<unsigned long long>(hi) << 32) | lo, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+                               (static_cast<unsigned long long>(hi + kDeqBias) << 32) | (lo + kDeqBias),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __builtin_amdgcn_s_waitcnt(0);
         }
     }

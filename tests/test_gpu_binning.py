@@ -285,3 +285,30 @@ def test_concurrent_contexts_config3(ramcrc, oracle_mod):
     finally:
         for c in ctxs:
             c.close()
+
+
+def test_long_phase_steals_on_sparse_batches(ctx, oracle_mod):
+    """Batches of a few long entries (0.5-60 KiB) among tiny ones: most of
+    k_entries' 256 workgroups own no octet of the long phase and steal from
+    the few that do, so deques are drained, over-drained by failing steals
+    and raced on.  Every CRC must still be exact, with and without initial
+    states, over many batches on one context (the round-5 deque bug -- an
+    over-drained back wrapping below the front -- claimed octets past the
+    table)."""
+    rng = np.random.default_rng(77)
+    total = 8 << 20
+    host = oracle_mod.splitmix_bytes(5, total)
+    base = dev(host)
+    for k in range(24):
+        n = int(rng.integers(1, 300))
+        lens = rng.integers(0, 120, n)
+        nlong = int(rng.integers(1, 12))
+        lens[rng.integers(0, n, nlong)] = rng.integers(500, 60000, nlong)
+        offs = rng.integers(0, total - 60000, n)
+        init = None if k % 2 else rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+        for api in ("entries", "batch"):
+            got = host_u32(run(ctx, api, base, offs, lens, init))
+            want = oracle_mod.entries(host, offs, lens, init=init)
+            bad = np.nonzero(got != want)[0]
+            assert bad.size == 0, (k, api, [(int(offs[i]) % 128, int(lens[i])) for i in bad[:8]])
+    ctx.check()

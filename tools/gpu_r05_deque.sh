@@ -6,7 +6,7 @@ O=gpurun_out/r05/deque
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
-    tests/test_gpu_parity.py tests/test_gpu_binning.py tests/test_gpu_segments.py tests/test_gpu_write_path.py \
+    tests/test_gpu_binning.py tests/test_gpu_parity.py tests/test_gpu_segments.py tests/test_gpu_write_path.py \
     tests/test_gpu_replay_fused.py tests/test_gpu_segment_ref.py > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 RAMCRC_LIB=ramcloud_amd/lib/variants/libramcrc_stamps.so timeout -k 10 200 python tools/stamps.py --save $O/mix.npy > $O/stamps_mix.txt 2>&1 || exit 1
