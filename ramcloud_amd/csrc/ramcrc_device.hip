@@ -998,6 +998,10 @@ constexpr int kAgeSkew = RAMCRC_AGE_SKEW, kAgeSkewRec = RAMCRC_AGE_SKEW_REC;
 #endif
 constexpr int kMaxDeq = 256;       // k_entries workgroups the deques cover (one per CU)
 constexpr uint32_t kDeqBias = 0x80000000u;   // both deque halves (see the long phase)
+#ifndef RAMCRC_DYN_STATIC
+#define RAMCRC_DYN_STATIC 75   // % of a workgroup's long-phase range split statically among its waves
+#endif
+constexpr uint64_t kDynStatic = RAMCRC_DYN_STATIC;
 #ifndef RAMCRC_STEAL_PROBES
 #define RAMCRC_STEAL_PROBES 8   // victims a workgroup tries once its own deque is empty
 #endif
@@ -3319,44 +3323,89 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
                 t = take(victim, true);
             }
         };
-        uint32_t mi = 0;   // nonempty bin of the last octet located
         u32x4 nd = {0u, 0u, 0u, 0u};
         uint32_t nix = kNoIdx, ninit = 0xFFFFFFFFu;
         int nbin = 0;
         const uint32_t ND = opre[nne];
+        // the bin of the last octet located, kept in scalars: consecutive
+        // claims almost always fall in it, so the LDS lookups happen per bin
+        uint32_t c_lo = 1, c_hi = 0, c_bin = 0;
+        uint64_t c_sb = 0;
         auto fetch = [&](uint32_t j) {
             if (j >= ND) {   // never (resolve validates every index); no load past the table
                 nd = u32x4{0u, 0u, 0u, 0u};
                 nix = kNoIdx;
                 return;
             }
-            if (j < opre[mi])
-                mi = 0;
-            while (j >= opre[mi + 1])
-                mi++;
-            mi = __builtin_amdgcn_readfirstlane(mi);
-            nbin = __builtin_amdgcn_readfirstlane(uint32_t(obin[mi]));
-            const uint64_t sl = s_start[nbin] + uint64_t(j - opre[mi]) * kG + g;
+            if (j < c_lo || j >= c_hi) {
+                uint32_t mi = 0;
+                while (j >= opre[mi + 1])
+                    mi++;
+                mi = __builtin_amdgcn_readfirstlane(mi);
+                c_lo = __builtin_amdgcn_readfirstlane(opre[mi]);
+                c_hi = __builtin_amdgcn_readfirstlane(opre[mi + 1]);
+                c_bin = __builtin_amdgcn_readfirstlane(uint32_t(obin[mi]));
+                c_sb = s_start[c_bin];
+            }
+            nbin = int(c_bin);
+            const uint64_t sl = c_sb + uint64_t(j - c_lo) * kG + g;
             nd = so.desc[sl];
             nix = so.idx[sl];
             if (d.init)
                 ninit = so.init[sl];
         };
-        uint32_t j = resolve(take(blk, false));
+        // The first kDynStatic % of the workgroup's range is split among its
+        // waves as the static form splits it (age-weighted, no atomics); the
+        // rest is the deque.  A wave takes its static octets, then claims.  A
+        // claim's atomic sits in the same in-order memory counter as the
+        // octet's data loads, so each one adds its latency to the next wait:
+        // claims only for the tail keep that off most octets.
+        const uint32_t sp = own_lo + uint32_t(uint64_t(own_hi - own_lo) * kDynStatic / 100);
+        const uint32_t slot = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
+        const int skew = d.vstat ? kAgeSkewRec : kAgeSkew;
+        auto cum = [&](uint32_t sl) -> uint64_t {
+            uint64_t c = 0;
+#pragma unroll
+            for (uint32_t r = 0; r < kEntWaves / 4; r++) {
+                const uint32_t n = sl > 4 * r ? (sl - 4 * r < 4 ? sl - 4 * r : 4) : 0;
+                c += uint64_t(n) * age_weight(r, skew);
+            }
+            return c;
+        };
+        const uint64_t tot = cum(kEntWaves);
+        uint32_t sj = own_lo + uint32_t(uint64_t(sp - own_lo) * cum(slot) / tot);
+        const uint32_t se = own_lo + uint32_t(uint64_t(sp - own_lo) * cum(slot + 1) / tot);
         unsigned long long t = 0;
-        if (j != kNoOct) {
+        bool ticket = false;
+        auto claim_next = [&]() -> uint32_t {
+            if (sj < se) {
+                const uint32_t o = sj++;
+                if (sj == se) {   // the claims start one octet ahead
+                    t = take(victim, steal);
+                    ticket = true;
+                }
+                return o;
+            }
+            if (!ticket)
+                t = take(victim, steal);   // (an empty static share)
+            ticket = false;
+            const uint32_t o = resolve(t);
+            if (o != kNoOct) {
+                t = take(victim, steal);
+                ticket = true;
+            }
+            return o;
+        };
+        uint32_t j = claim_next();
+        if (j != kNoOct)
             fetch(j);
-            t = take(victim, steal);
-        }
         while (j != kNoOct) {
             const u32x4 dd = nd;
             const uint32_t ix = nix, init = ninit;
             const int b = nbin;
-            const uint32_t jn = resolve(t);   // issued one octet ago
-            if (jn != kNoOct) {
+            const uint32_t jn = claim_next();   // a claim issued one octet ago
+            if (jn != kNoOct)
                 fetch(jn);   // the next octet's descriptor, before this octet runs
-                t = take(victim, steal);
-            }
             octet(dd, ix, init, b);
             j = jn;
         }
@@ -3541,8 +3590,10 @@ __global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc 
                 const uint64_t ib = so.bt->items[b], cost = so.bt->kcost[b];
                 return opre[m] + (p > ib ? uint32_t((p - ib + cost - 1) / cost) : 0u);
             };
-            const uint32_t lo = oct_at(I0 + T * blockIdx.x / gridDim.x);
+            const uint32_t lo0 = oct_at(I0 + T * blockIdx.x / gridDim.x);
             const uint32_t hi = oct_at(I0 + T * (blockIdx.x + 1) / gridDim.x);
+            // the waves' static shares come first; the deque holds the rest
+            const uint32_t lo = lo0 + uint32_t(uint64_t(hi - lo0) * kDynStatic / 100);
             __hip_atomic_store(&so.bt->ctr[so.par].deq[blockIdx.x],
                                (static_cast<unsigned long long>(hi + kDeqBias) << 32) | (lo + kDeqBias),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
