@@ -216,13 +216,6 @@ constexpr uint32_t kHeadOff = kXinvOff + 1024;            // k_entries: head mas
 constexpr uint32_t kTailOff = kHeadOff + 21 * 32;         // k_entries: tail masks (272 B)
 constexpr uint32_t kBinOff = kTailOff + 17 * 16;          // k_entries: bin table (4 KiB)
 constexpr uint32_t kLdsEntries = kBinOff + 4096;          // 157616 B
-// the long phase's dynamic octet order (RAMCRC_LONG_DYN), after the bin table
-// (items 1296 B, starts 1288 B, costs 644 B) in the same 4 KiB
-constexpr uint32_t kDynPreOff = kBinOff + 3232;           // octets before each nonempty long bin (162 x 4 B)
-constexpr uint32_t kDynBinOff = kDynPreOff + 162 * 4;     // the nonempty long bins, ascending (161 B)
-constexpr uint32_t kDynNneOff = kDynBinOff + 164;         // their number (4 B)
-constexpr uint32_t kDynVicOff = kDynNneOff + 4;           // workgroup: next steal victim (4 B)
-static_assert(kDynVicOff + 4 <= kLdsEntries, "dynamic order fits the bin table's 4 KiB");
 static_assert(kBinOff % 16 == 0, "LDS table alignment");
 static_assert(kBinOff - kX4Off == sizeof(DeviceTables::LongTabs), "long-phase tables: LDS = g_tab.lt");
 static_assert(kLdsEntries <= 160 * 1024, "LDS budget");
@@ -977,6 +970,13 @@ constexpr int kPU = RAMCRC_PU;             // ping-pong depth (pipelined bins)
 #define RAMCRC_TINY_PROBE 0  // A/B only: conflict-free lookup addresses, wrong CRCs
 #endif
 constexpr uint32_t kNoIdx = 0xFFFFFFFFu;   // empty slot
+#ifndef RAMCRC_SPLIT
+#define RAMCRC_SPLIT 1   // k_entries: tiny and long phases on separate workgroups when a batch has both
+#endif
+#ifndef RAMCRC_SPLIT_KAPPA
+#define RAMCRC_SPLIT_KAPPA 256   // a tiny window in long-phase work units, x 1024
+#endif
+constexpr uint64_t kSplitKappa = RAMCRC_SPLIT_KAPPA;
 #ifndef RAMCRC_OCTET_COST
 #define RAMCRC_OCTET_COST 4
 #endif
@@ -993,18 +993,6 @@ constexpr uint64_t kOctetCost = RAMCRC_OCTET_COST;   // per-octet overhead in st
 // to skew 120-160 (config-3 mix +4 % over 80), replay verify (records mode)
 // loses from 120 on (-3 %), so records mode keeps 80.
 constexpr int kAgeSkew = RAMCRC_AGE_SKEW, kAgeSkewRec = RAMCRC_AGE_SKEW_REC;
-#ifndef RAMCRC_LONG_DYN
-#define RAMCRC_LONG_DYN 1   // long bins: per-workgroup octet deques with stealing (0: static shares)
-#endif
-constexpr int kMaxDeq = 256;       // k_entries workgroups the deques cover (one per CU)
-constexpr uint32_t kDeqBias = 0x80000000u;   // both deque halves (see the long phase)
-#ifndef RAMCRC_DYN_STATIC
-#define RAMCRC_DYN_STATIC 75   // % of a workgroup's long-phase range split statically among its waves
-#endif
-constexpr uint64_t kDynStatic = RAMCRC_DYN_STATIC;
-#ifndef RAMCRC_STEAL_PROBES
-#define RAMCRC_STEAL_PROBES 8   // victims a workgroup tries once its own deque is empty
-#endif
 __host__ __device__ constexpr uint64_t age_weight(uint32_t r, int skew)
 {
     return uint64_t(2000 + skew * (3 - 2 * int(r)));
@@ -1020,9 +1008,6 @@ constexpr int kBinPer = RAMCRC_BIN_PER;    // entries per thread per tile (count
 #ifndef RAMCRC_BIN_RESCUE
 #define RAMCRC_BIN_RESCUE 1   // the guarded scatter after every k_bin_one (A/B only: 0 = none,
                               // an aborted k_bin_one then leaves its batch unbinned)
-#endif
-#ifndef RAMCRC_RESCUE_WGS
-#define RAMCRC_RESCUE_WGS 32   // guarded scatter's grid cap (0: one workgroup per tile)
 #endif
 #ifndef RAMCRC_BIN_SLICES
 #define RAMCRC_BIN_SLICES 8   // k_bin_one: histogram copies (workgroup i adds to copy i % 8: its XCD's)
@@ -1116,7 +1101,6 @@ struct BinCounters {
     uint32_t pad_;
     uint32_t hs[kBinSlices][kNB];   // k_bin_one: histogram per slice of workgroups
     uint32_t arr[kBinSlices];       // k_bin_one: arrivals per slice
-    unsigned long long deq[kMaxDeq];   // k_entries' long phase: per workgroup, back << 32 | front
 };
 
 constexpr uint32_t kBinGo = 1, kBinAbort = 2;   // BinCounters::flag: k_bin_one's vote
@@ -1243,8 +1227,6 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
             nx.hs[t / kNB][t % kNB] = 0;
         for (int t = threadIdx.x; t < kBinSlices; t += blockDim.x)
             nx.arr[t] = 0;
-        for (int t = threadIdx.x; t < kMaxDeq; t += blockDim.x)
-            nx.deq[t] = 0;
         if (threadIdx.x == 0) {
             nx.nlarge = 0;
             nx.ninact = 0;
@@ -1679,8 +1661,6 @@ __global__ __launch_bounds__(kThreads) void k_bin_one(BatchDesc d, Sorted so, in
             nx.hs[t / kNB][t % kNB] = 0;
         for (int t = threadIdx.x; t < kBinSlices; t += blockDim.x)
             nx.arr[t] = 0;
-        for (int t = threadIdx.x; t < kMaxDeq; t += blockDim.x)
-            nx.deq[t] = 0;
         if (threadIdx.x == 0) {
             nx.nlarge = 0;
             nx.ninact = 0;
@@ -3239,176 +3219,6 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
     // 1-2 us per chunk; DESIGN.md section 5.4, profiles/r03/long.)
     if constexpr (kSmall) {
         run(I0 + T * wave / nwaves, I0 + T * (wave + 1) / nwaves);
-    } else if (RAMCRC_LONG_DYN != 0 && nblk <= uint32_t(kMaxDeq)) {
-        // Work-stealing deques (round 5).  Static shares left the waves of
-        // the config-3 mix ending between 160 and 218 us (phase stamps,
-        // profiles/r05/stamps): inside a workgroup the SIMDs favour old waves
-        // by more than a fixed skew matches, and between workgroups the same
-        // work estimate ran 160-175 us depending on where in the bins it lay.
-        // Workgroup blk owns the same contiguous range of octets its static
-        // share covered (octets numbered in bin order, a range = the octets
-        // whose first work unit lies in the share), as a deque in one 64-bit
-        // device word, back << 32 | front.  Its waves take octets from the
-        // front, one atomic add each, issued one octet ahead; a workgroup
-        // whose deque is empty steals single octets from the back of other
-        // workgroups' deques (subtracting 1 << 32).  Owner and thief never
-        // both get an octet: the atomic that moves front past back, or back to
-        // front, sees an empty range.  Both halves are biased by 2^31
-        // (kDeqBias), so the failing steals that keep decrementing an empty
-        // deque's back can never wrap it below its front (an unbiased back of
-        // 3 reached 0xFFFFFFFF after four of them, the empty deque looked full
-        // and its owner claimed octets past the table: an illegal address on
-        // the first GPU run of this form).  Octets stay in address order within a
-        // workgroup's range, which the interleaved form of this (8 counters
-        // over a global largest-first order) lost: it balanced the waves to
-        // 3 us but ran 1.2-1.5x slower (profiles/r05/longdyn/ab_long.txt).
-        constexpr uint32_t kNoOct = 0xFFFFFFFFu;
-        const uint32_t* opre = reinterpret_cast<const uint32_t*>(lds + kDynPreOff);
-        const uint8_t* obin = lds + kDynBinOff;
-        uint32_t* vic = reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(lds) + kDynVicOff);
-        const uint32_t nne = *reinterpret_cast<const uint32_t*>(lds + kDynNneOff);
-        unsigned long long* deq = so.bt->ctr[so.par].deq;
-        // octets whose first work unit lies below item p
-        auto oct_at = [&](uint64_t p) -> uint32_t {
-            uint32_t m = 0;
-            while (m < nne && s_items[obin[m] + 1] <= p)
-                m++;
-            if (m == nne)
-                return opre[nne];
-            const int b = obin[m];
-            const uint64_t ib = s_items[b];
-            const uint32_t o = p > ib ? uint32_t((p - ib + s_cost[b] - 1) / s_cost[b]) : 0u;
-            return opre[m] + o;
-        };
-        auto range_of = [&](uint32_t k, uint32_t& lo, uint32_t& hi) {
-            lo = __builtin_amdgcn_readfirstlane(oct_at(I0 + T * k / nblk));
-            hi = __builtin_amdgcn_readfirstlane(oct_at(I0 + T * (k + 1) / nblk));
-        };
-        // the deque of this workgroup was initialised by its wave 0 before the
-        // phase's barrier (k_entries); a ticket is the old word of an atomic add
-        auto take = [&](uint32_t v, bool steal) -> unsigned long long {
-            unsigned long long t = 0;
-            if (lane == 0)
-                t = __hip_atomic_fetch_add(&deq[v], steal ? 0xFFFFFFFF00000000ull : 1ull,
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return t;
-        };
-        uint32_t victim = blk;   // whose deque the ticket is on
-        bool steal = false;
-        uint32_t vlo = 0, vhi = 0;   // the victim's range (a stolen octet must lie in it)
-        uint32_t own_lo, own_hi;
-        range_of(blk, own_lo, own_hi);
-        // the octet a ticket stands for; kNoOct when this workgroup is done
-        auto resolve = [&](unsigned long long t) -> uint32_t {
-            for (;;) {
-                const uint32_t f = __builtin_amdgcn_readfirstlane(uint32_t(t));
-                const uint32_t bk = __builtin_amdgcn_readfirstlane(uint32_t(t >> 32));
-                if (f < bk) {
-                    const uint32_t o = (steal ? bk - 1 : f) - kDeqBias;
-                    // (a victim's deque not yet set up holds no valid range)
-                    if (o >= (steal ? vlo : own_lo) && o < (steal ? vhi : own_hi))
-                        return o;
-                }
-                // this deque is empty: the next victim (shared by the workgroup's waves)
-                uint32_t k = 0;
-                if (lane == 0)
-                    k = atomicAdd(vic, 1u);
-                k = __builtin_amdgcn_readfirstlane(k);
-                if (k >= uint32_t(RAMCRC_STEAL_PROBES) || k + 1 >= nblk)
-                    return kNoOct;
-                // victims spread over the grid: blk + 1, + 3, + 7, ...
-                victim = (blk + ((2u << k) - 1)) % nblk;
-                steal = true;
-                range_of(victim, vlo, vhi);
-                t = take(victim, true);
-            }
-        };
-        u32x4 nd = {0u, 0u, 0u, 0u};
-        uint32_t nix = kNoIdx, ninit = 0xFFFFFFFFu;
-        int nbin = 0;
-        const uint32_t ND = opre[nne];
-        // the bin of the last octet located, kept in scalars: consecutive
-        // claims almost always fall in it, so the LDS lookups happen per bin
-        uint32_t c_lo = 1, c_hi = 0, c_bin = 0;
-        uint64_t c_sb = 0;
-        auto fetch = [&](uint32_t j) {
-            if (j >= ND) {   // never (resolve validates every index); no load past the table
-                nd = u32x4{0u, 0u, 0u, 0u};
-                nix = kNoIdx;
-                return;
-            }
-            if (j < c_lo || j >= c_hi) {
-                uint32_t mi = 0;
-                while (j >= opre[mi + 1])
-                    mi++;
-                mi = __builtin_amdgcn_readfirstlane(mi);
-                c_lo = __builtin_amdgcn_readfirstlane(opre[mi]);
-                c_hi = __builtin_amdgcn_readfirstlane(opre[mi + 1]);
-                c_bin = __builtin_amdgcn_readfirstlane(uint32_t(obin[mi]));
-                c_sb = s_start[c_bin];
-            }
-            nbin = int(c_bin);
-            const uint64_t sl = c_sb + uint64_t(j - c_lo) * kG + g;
-            nd = so.desc[sl];
-            nix = so.idx[sl];
-            if (d.init)
-                ninit = so.init[sl];
-        };
-        // The first kDynStatic % of the workgroup's range is split among its
-        // waves as the static form splits it (age-weighted, no atomics); the
-        // rest is the deque.  A wave takes its static octets, then claims.  A
-        // claim's atomic sits in the same in-order memory counter as the
-        // octet's data loads, so each one adds its latency to the next wait:
-        // claims only for the tail keep that off most octets.
-        const uint32_t sp = own_lo + uint32_t(uint64_t(own_hi - own_lo) * kDynStatic / 100);
-        const uint32_t slot = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
-        const int skew = d.vstat ? kAgeSkewRec : kAgeSkew;
-        auto cum = [&](uint32_t sl) -> uint64_t {
-            uint64_t c = 0;
-#pragma unroll
-            for (uint32_t r = 0; r < kEntWaves / 4; r++) {
-                const uint32_t n = sl > 4 * r ? (sl - 4 * r < 4 ? sl - 4 * r : 4) : 0;
-                c += uint64_t(n) * age_weight(r, skew);
-            }
-            return c;
-        };
-        const uint64_t tot = cum(kEntWaves);
-        uint32_t sj = own_lo + uint32_t(uint64_t(sp - own_lo) * cum(slot) / tot);
-        const uint32_t se = own_lo + uint32_t(uint64_t(sp - own_lo) * cum(slot + 1) / tot);
-        unsigned long long t = 0;
-        bool ticket = false;
-        auto claim_next = [&]() -> uint32_t {
-            if (sj < se) {
-                const uint32_t o = sj++;
-                if (sj == se) {   // the claims start one octet ahead
-                    t = take(victim, steal);
-                    ticket = true;
-                }
-                return o;
-            }
-            if (!ticket)
-                t = take(victim, steal);   // (an empty static share)
-            ticket = false;
-            const uint32_t o = resolve(t);
-            if (o != kNoOct) {
-                t = take(victim, steal);
-                ticket = true;
-            }
-            return o;
-        };
-        uint32_t j = claim_next();
-        if (j != kNoOct)
-            fetch(j);
-        while (j != kNoOct) {
-            const u32x4 dd = nd;
-            const uint32_t ix = nix, init = ninit;
-            const int b = nbin;
-            const uint32_t jn = claim_next();   // a claim issued one octet ago
-            if (jn != kNoOct)
-                fetch(jn);   // the next octet's descriptor, before this octet runs
-            octet(dd, ix, init, b);
-            j = jn;
-        }
     } else {
         const uint64_t P0 = I0 + T * blk / nblk, PT = I0 + T * (blk + 1) / nblk - P0;
         const uint32_t slot = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
@@ -3488,11 +3298,40 @@ __device__ __forceinline__ void entries_run(const BatchDesc& d, const Sorted& so
         flush_batch();
 }
 
+// The long-phase tables into the LDS, then the short and the long bins over
+// workgroups blk of nblk.  Refuses (status bits) on an inconsistent layout.
+__device__ __forceinline__ void long_phase(const BatchDesc& d, const Sorted& so, uint8_t* lds, bool bad,
+                                           uint32_t blk, uint32_t nblk)
+{
+    fill_long(lds);
+    uint64_t* s_items = reinterpret_cast<uint64_t*>(lds + kBinOff);   // kNB + 1
+    uint64_t* s_start = s_items + (kNB + 1);                          // kNB
+    uint32_t* s_cost = reinterpret_cast<uint32_t*>(s_start + kNB);    // kNB
+    for (int t = threadIdx.x; t <= kNB; t += blockDim.x) {
+        s_items[t] = so.bt->items[t];
+        if (t < kNB) {
+            s_start[t] = so.bt->start[t];
+            s_cost[t] = uint32_t(so.bt->kcost[t]);
+        }
+    }
+    if (__syncthreads_or(bad)) {
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            atomicOr(so.status, kStatusSticky | kStatusBins);
+        return;
+    }
+    RAMCRC_STAMP(2);
+    entries_run<true>(d, so, lds, blk, nblk);
+    RAMCRC_STAMP(3);
+    entries_run<false>(d, so, lds, blk, nblk);
+    RAMCRC_STAMP(4);
+}
+
 // Both phases in one launch (one LDS fill, one launch boundary): the exact
 // short bins, then the pipelined long bins.  The phases are separate inlined
 // loops, so the long-entry loop's registers are not shared with the short one.
 __global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc d, Sorted so)
 {
+    static_assert(RAMCRC_TINY_CF, "k_entries runs the conflict-free tiny phases");
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsEntries];
     // Every bin must hold exactly the entries the scatter placed in it
     // (cursor == count): then every sorted slot this launch reads was written
@@ -3506,110 +3345,48 @@ __global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc 
         if (blockIdx.x == 0 && threadIdx.x == 0)
             atomicOr(so.status, kStatusSticky | kStatusBins);
     };
-#if RAMCRC_TINY_CF
     RAMCRC_STAMP(0);
     const bool have_tk = kTinyK >= 2 && !so.bt->direct_n && so.bt->start[kTinyK + 1] != so.bt->start[2];
-    bool tiny_ok = tiny_run_cf(d, so, lds, bad, blockIdx.x, gridDim.x, have_tk);
-    if (tiny_ok && have_tk)
-        tiny_multi(d, so, lds, blockIdx.x, gridDim.x);
+    // Role split (round 5, RAMCRC_SPLIT): when a batch has both tiny and long
+    // entries, workgroups < T run only the tiny phases (filling only their
+    // table) and the others only the long phase, so the two overlap and no
+    // workgroup waits for its slowest tiny wave before refilling its LDS.  T
+    // follows the work: a tiny window costs kSplitKappa / 1024 long-phase work
+    // units.  T = 0: both phases on every workgroup, in sequence.
+    uint32_t T = 0;
+    constexpr int kT = kTinyK > kSmallK ? kTinyK : kSmallK;
+    if (RAMCRC_SPLIT && !so.bt->direct_n && so.bt->start[kTinyK + 1] != so.bt->start[0] &&
+        so.bt->items[kNB] != so.bt->items[kT + 1]) {
+        uint64_t win = so.bt->start[2] - so.bt->start[0];   // one window each
+        for (int b = 2; b <= kTinyK; b++)
+            win += (so.bt->start[b + 1] - so.bt->start[b]) * uint64_t(b);
+        const uint64_t ct = win * kSplitKappa / 1024, cl = so.bt->items[kNB] - so.bt->items[kT + 1];
+        T = uint32_t((uint64_t(gridDim.x) * ct + (ct + cl) / 2) / (ct + cl));
+        T = T < 1 ? 1 : (T > gridDim.x - 1 ? gridDim.x - 1 : T);
+    }
+    const bool do_tiny = T == 0 || blockIdx.x < T, do_long = T == 0 || blockIdx.x >= T;
+    const uint32_t tn = T ? T : gridDim.x;
+    bool tiny_ok = true;
+    if (do_tiny) {
+        tiny_ok = tiny_run_cf(d, so, lds, bad, blockIdx.x, tn, have_tk);
+        if (tiny_ok && have_tk)
+            tiny_multi(d, so, lds, blockIdx.x, tn);
+    }
     RAMCRC_STAMP(1);
-#else
-    const bool tiny_ok = tiny_run(d, so, lds, bad, blockIdx.x, gridDim.x);
-#endif
     if (!tiny_ok) {
         refuse();
         return;
     }
+    if (!do_long)
+        return;
     if (so.bt->items[2] == so.bt->items[kNB]) {   // every entry is tiny (or large on the batch path)
         if (__syncthreads_or(bad))
             refuse();
         return;
     }
-    // The position table is dead: refill the LDS.  (Splitting the grid
-    // between the two phases instead -- no barrier, no refill -- measured
-    // within 1 % on the config-3 mix and was dropped, profiles/r03/ab.)
+    // the position table is dead (when this workgroup ran the tiny phases)
     __syncthreads();
-    fill_long(lds);
-    uint64_t* s_items = reinterpret_cast<uint64_t*>(lds + kBinOff);   // kNB + 1
-    uint64_t* s_start = s_items + (kNB + 1);                          // kNB
-    uint32_t* s_cost = reinterpret_cast<uint32_t*>(s_start + kNB);    // kNB
-    for (int t = threadIdx.x; t <= kNB; t += blockDim.x) {
-        s_items[t] = so.bt->items[t];
-        if (t < kNB) {
-            s_start[t] = so.bt->start[t];
-            s_cost[t] = uint32_t(so.bt->kcost[t]);
-        }
-    }
-#if RAMCRC_LONG_DYN
-    if (threadIdx.x < kWaveSize && gridDim.x <= kMaxDeq) {
-        // the long phase's octet numbering: nonempty long bins in ascending
-        // order with the octets before each; then this workgroup's deque
-        // (wave 0; the barrier below publishes both to the workgroup)
-        constexpr int kT = kTinyK > kSmallK ? kTinyK : kSmallK;
-        uint32_t* opre = reinterpret_cast<uint32_t*>(lds + kDynPreOff);
-        uint8_t* obin = lds + kDynBinOff;
-        const int lane = threadIdx.x;
-        uint32_t carry = 0, base = 0;
-        for (int c = 0; c * kWaveSize < kNB - (kT + 1); c++) {
-            const int b = kT + 1 + c * kWaveSize + lane;
-            uint32_t oct = 0;
-            if (b < kNB) {
-                const uint64_t it = so.bt->items[b + 1] - so.bt->items[b];
-                oct = it ? uint32_t(it / so.bt->kcost[b]) : 0u;
-            }
-            const uint64_t ne = __ballot(oct != 0);
-            uint32_t ps = oct;
-#pragma unroll
-            for (int sft = 1; sft < kWaveSize; sft <<= 1) {
-                const uint32_t a = __shfl_up(ps, sft, kWaveSize);
-                if (lane >= sft)
-                    ps += a;
-            }
-            const uint32_t rank = uint32_t(__popcll(ne & ((1ull << lane) - 1)));
-            if (oct) {
-                obin[base + rank] = uint8_t(b);
-                opre[base + rank] = carry + ps - oct;
-            }
-            carry += __shfl(ps, kWaveSize - 1, kWaveSize);
-            base += uint32_t(__popcll(ne));
-        }
-        if (lane == 0) {
-            opre[base] = carry;
-            *reinterpret_cast<uint32_t*>(lds + kDynNneOff) = base;
-            *reinterpret_cast<uint32_t*>(lds + kDynVicOff) = 0u;
-            // this workgroup's share, as the static split cuts the work units
-            // (the same arithmetic as the long phase's range_of)
-            const uint64_t I0 = so.bt->items[kT + 1], T = so.bt->items[kNB] - I0;
-            auto oct_at = [&](uint64_t p) -> uint32_t {
-                uint32_t m = 0;
-                while (m < base && so.bt->items[obin[m] + 1] <= p)
-                    m++;
-                if (m == base)
-                    return carry;
-                const int b = obin[m];
-                const uint64_t ib = so.bt->items[b], cost = so.bt->kcost[b];
-                return opre[m] + (p > ib ? uint32_t((p - ib + cost - 1) / cost) : 0u);
-            };
-            const uint32_t lo0 = oct_at(I0 + T * blockIdx.x / gridDim.x);
-            const uint32_t hi = oct_at(I0 + T * (blockIdx.x + 1) / gridDim.x);
-            // the waves' static shares come first; the deque holds the rest
-            const uint32_t lo = lo0 + uint32_t(uint64_t(hi - lo0) * kDynStatic / 100);
-            __hip_atomic_store(&so.bt->ctr[so.par].deq[blockIdx.x],
-                               (static_cast<unsigned long long>(hi + kDeqBias) << 32) | (lo + kDeqBias),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_s_waitcnt(0);
-        }
-    }
-#endif
-    if (__syncthreads_or(bad)) {
-        refuse();
-        return;
-    }
-    RAMCRC_STAMP(2);
-    entries_run<true>(d, so, lds, blockIdx.x, gridDim.x);
-    RAMCRC_STAMP(3);
-    entries_run<false>(d, so, lds, blockIdx.x, gridDim.x);
-    RAMCRC_STAMP(4);
+    long_phase(d, so, lds, bad, blockIdx.x - T, gridDim.x - T);
 }
 
 // ------------------------------------------------------------ k_plan
@@ -4022,15 +3799,9 @@ int bin_finish(ramcrc_ctx* c, const BatchDesc& d, hipStream_t s, int skip_large,
         HIPCHK(hipGetLastError());
     }
     if (!so.one || RAMCRC_BIN_RESCUE) {
-        // after k_bin_one: the guarded scatter, which exits at once unless
-        // k_bin_one aborted -- on a smaller grid (grid-stride over the tiles),
-        // since every batch pays its dispatch and only an abort its work
-        uint64_t grid = bin_grid(c, d.n);
-        constexpr uint64_t kRescueWgs = RAMCRC_RESCUE_WGS;
-        if (so.one && kRescueWgs != 0 && grid > kRescueWgs)
-            grid = kRescueWgs;
-        hipLaunchKernelGGL(k_bin_scatter<kMode>, dim3(grid), dim3(kThreads), 0, s, d, so, skip_large,
-                           int(so.one));
+        // after k_bin_one: the guarded scatter (exits at once unless k_bin_one aborted)
+        hipLaunchKernelGGL(k_bin_scatter<kMode>, dim3(bin_grid(c, d.n)), dim3(kThreads), 0, s, d,
+                           so, skip_large, int(so.one));
         HIPCHK(hipGetLastError());
     }
     {
