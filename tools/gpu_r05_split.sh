@@ -8,6 +8,6 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method threa
     tests/test_gpu_binning.py tests/test_gpu_parity.py tests/test_gpu_segments.py tests/test_gpu_write_path.py \
     tests/test_gpu_replay_fused.py > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
-VARIANTS="sp0 kap128 kap512" CASES="--config entries;--config append;--config replay --value-len 128;--config entries --entry-size 1024" \
-    REPS=2 STEPS=20 TAG=r05/split/ab bash tools/gpu_ab.sh || exit 1
-python tools/ab_summary.py gpurun_out/r05/split/ab
+VARIANTS="sp0 kap192 kap320" CASES="--config entries;--config append;--config entries --entry-size 1024;--config entries --entry-size 4096" \
+    REPS=3 STEPS=20 TAG=r05/split/ab2 bash tools/gpu_ab.sh || exit 1
+python tools/ab_summary.py gpurun_out/r05/split/ab2
