@@ -1021,6 +1021,22 @@ constexpr int kBinSlices = RAMCRC_BIN_SLICES;
 #endif
 constexpr uint64_t kBinWgsPerCu = RAMCRC_BIN_WGS_PER_CU;   // binning grid cap per CU
 
+#ifndef RAMCRC_TINY_PF
+// tiny rounds: the next round's windows loaded into registers while this one
+// is hashed -- 0 never, 1 always, 2 records batches only (replay)
+#define RAMCRC_TINY_PF 2
+#endif
+#ifndef RAMCRC_TINY_LSEL
+// tiny windows: per-lane v_perm selectors instead of a v_alignbyte per dword
+// -- 0 never, 1 always, 2 where the round loop has no register prefetch
+#define RAMCRC_TINY_LSEL 2
+#endif
+#ifndef RAMCRC_TINY_T3
+#define RAMCRC_TINY_T3 1   // tiny windows: tail masks on dword 3 only when every window ends at >= 96
+#endif
+#ifndef RAMCRC_TINY_MED3
+#define RAMCRC_TINY_MED3 1   // tiny window tail clamp as one v_med3 per dword
+#endif
 #ifndef RAMCRC_TINY_HM
 #define RAMCRC_TINY_HM 1   // 8-lane group XOR: third step by DPP row_half_mirror (0: ds_swizzle)
 #endif
@@ -2362,11 +2378,27 @@ struct TwRows {
 };
 #endif
 
+// Per-lane v_perm selectors for tiny_win_wr<true>: lookup k of a dword takes
+// its byte (k + g4) & 3 straight into address bits 8-15, which replaces the
+// v_alignbyte rotation per dword (4 VGPRs for 32 VALU per round).
+struct TwSel {
+    uint32_t sel[4];
+    __device__ TwSel() {}
+    __device__ explicit TwSel(uint32_t g4)
+    {
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            sel[k] = 0x0C020000u | ((4u + ((uint32_t(k) + g4) & 3)) << 8);
+    }
+};
+
 // The group's sum over one window's bytes in [sa, e), byte b at position o
 // as X^(128 - o)(b) (relative to the window's end; all 8 lanes get it).
 #if RAMCRC_TINY_LD16
+template <bool kLsel = false, bool kTail3 = false>
 __device__ __forceinline__ uint32_t tiny_win_wr(const uint8_t* lds, const u32x4& wv, uint32_t sa,
-                                                uint32_t e, const TwRows& rw, uint32_t gl, uint32_t g4)
+                                                uint32_t e, const TwRows& rw, uint32_t gl, uint32_t g4,
+                                                const TwSel& = TwSel())
 {
     // this group's dword order: instruction j takes dword (j + g4) & 3
     const uint32_t w0 = wv.x, w1 = wv.y, w2 = wv.z, w3 = wv.w;
@@ -2397,8 +2429,12 @@ __device__ __forceinline__ uint32_t tiny_win_wr(const uint8_t* lds, const u32x4&
     return R;
 }
 #else
+// kTail3: the caller knows e >= 96 for every window of the wave, so dwords
+// 0-2 (window offsets below 96) need no tail mask
+template <bool kLsel = false, bool kTail3 = false>
 __device__ __forceinline__ uint32_t tiny_win_wr(const uint8_t* lds, const u32x4& wv, uint32_t sa,
-                                                uint32_t e, const TwRows& rw, uint32_t gl, uint32_t g4)
+                                                uint32_t e, const TwRows& rw, uint32_t gl, uint32_t g4,
+                                                const TwSel& ts = TwSel())
 {
     // tail: dword j keeps its bytes before e, clamp(e - 32 j - 4 u, 0, 4)
     const int z = 32 - 8 * int(e) + 32 * int(gl);   // bits to drop from dword 0's top
@@ -2408,17 +2444,35 @@ __device__ __forceinline__ uint32_t tiny_win_wr(const uint8_t* lds, const u32x4&
     uint32_t v[16];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-        const uint32_t sh = uint32_t(min(max(z + 256 * j, 0), 32));
-        uint32_t keep = uint32_t(uint64_t(0xFFFFFFFFu) >> sh);
+        uint32_t keep = 0xFFFFFFFFu;
+        if (!kTail3 || j == 3) {
+#if RAMCRC_TINY_MED3
+            // one v_med3 after the add (the compiler's max/add/min is three ops)
+            uint32_t sh;
+            asm("v_med3_i32 %0, %1, 0, 32" : "=v"(sh) : "v"(z + 256 * j));
+#else
+            const uint32_t sh = uint32_t(min(max(z + 256 * j, 0), 32));
+#endif
+            keep = uint32_t(uint64_t(0xFFFFFFFFu) >> sh);
+        }
         if (j == 0)
             keep &= uint32_t(~uint64_t(0) << hd);
         const uint32_t xb = ws[j] & keep;
-        const uint32_t xr = __builtin_amdgcn_alignbyte(xb, xb, g4);   // conflict-free banks
+        if constexpr (kLsel) {
+            // lookup k takes byte (k + g4) & 3 (conflict-free banks) through
+            // the lane's own selector instead of a rotated copy of the dword
 #pragma unroll
-        for (int k = 0; k < 4; k++)
-            v[4 * j + k] = *reinterpret_cast<const uint32_t*>(
-                lds + __builtin_amdgcn_perm(xr, rw.lr[j >> 1][k], 0x0C020000u | ((4u + uint32_t(k)) << 8)) +
-                128 * (j & 1));
+            for (int k = 0; k < 4; k++)
+                v[4 * j + k] = *reinterpret_cast<const uint32_t*>(
+                    lds + __builtin_amdgcn_perm(xb, rw.lr[j >> 1][k], ts.sel[k]) + 128 * (j & 1));
+        } else {
+            const uint32_t xr = __builtin_amdgcn_alignbyte(xb, xb, g4);   // conflict-free banks
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                v[4 * j + k] = *reinterpret_cast<const uint32_t*>(
+                    lds + __builtin_amdgcn_perm(xr, rw.lr[j >> 1][k], 0x0C020000u | ((4u + uint32_t(k)) << 8)) +
+                    128 * (j & 1));
+        }
     }
     const uint32_t t0 = xor3(v[0], v[1], v[2]), t1 = xor3(v[3], v[4], v[5]);
     const uint32_t t2 = xor3(v[6], v[7], v[8]), t3 = xor3(v[9], v[10], v[11]);
@@ -2454,6 +2508,7 @@ __device__ __forceinline__ uint32_t tw_inv128(const uint8_t* lds, uint32_t v)
     return xor3(t(0, v & 0xFF), t(1, (v >> 8) & 0xFF), t(2, (v >> 16) & 0xFF)) ^ t(3, v >> 24);
 }
 
+template <bool kPF>
 __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so, uint8_t* lds,
                                             bool bad, uint32_t blk, uint32_t nblk, bool need_table)
 {
@@ -2587,6 +2642,11 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
 #if RAMCRC_TINY_WR
     tiny_fill(lds);
     const TwRows rw(gl, g4);
+    // without the register prefetch the selectors fit (RAMCRC_TINY_LSEL 2)
+    constexpr bool kLsel = RAMCRC_TINY_LSEL == 2 ? !kPF : bool(RAMCRC_TINY_LSEL);
+    TwSel ts;
+    if constexpr (kLsel)
+        ts = TwSel(g4);
 #else
     fill_plain(lds, 0, g_tab.post, 256 * 128 + 128);
 #endif
@@ -2601,15 +2661,21 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
         const TinyOwn o2 = load_own(r + 2 * nwaves);
         u32x4 wn[8];
         uint32_t gn[8], sn = 0;
-        if (r + nwaves < rounds)
-            issue(o1, wn, gn, sn);
+        if constexpr (kPF) {
+            if (r + nwaves < rounds)
+                issue(o1, wn, gn, sn);
+        }
         uint32_t mine = 0;
 #if RAMCRC_TINY_WR
 #pragma unroll
         for (int q = 0; q < 8; q++) {
             const uint32_t sa = (gc[q] >> 8) & 0xF;
             const uint32_t e = sa + (gc[q] & 0xFF);           // window-relative end, <= 128
-            const uint32_t R = tiny_win_wr(lds, wc[q], sa, e, rw, gl, g4);
+            // (a wave-uniform branch: entries of 81 B or more skip most tail masks)
+            // (not with the register prefetch: its loop has no VGPRs to spare)
+            const bool t3 = RAMCRC_TINY_T3 && !kPF && __builtin_amdgcn_ballot_w64(e < 96) == 0;
+            const uint32_t R = t3 ? tiny_win_wr<kLsel, true>(lds, wc[q], sa, e, rw, gl, g4, ts)
+                                  : tiny_win_wr<kLsel, false>(lds, wc[q], sa, e, rw, gl, g4, ts);
             mine = gl == uint32_t(q) ? R : mine;
         }
 #else
@@ -2690,11 +2756,18 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
         RAMCRC_STAMP_ONCE(6, first_round);
         o0 = o1;
         o1 = o2;
-        sc = sn;
+        if constexpr (kPF) {
+            sc = sn;
 #pragma unroll
-        for (int q = 0; q < 8; q++) {
-            wc[q] = wn[q];
-            gc[q] = gn[q];
+            for (int q = 0; q < 8; q++) {
+                wc[q] = wn[q];
+                gc[q] = gn[q];
+            }
+        } else {
+            // the next round's windows straight into the spent buffer: the
+            // other waves of the SIMD cover their latency
+            if (r + nwaves < rounds)
+                issue(o0, wc, gc, sc);
         }
     }
     return true;
@@ -3368,7 +3441,11 @@ __global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc 
     const uint32_t tn = T ? T : gridDim.x;
     bool tiny_ok = true;
     if (do_tiny) {
-        tiny_ok = tiny_run_cf(d, so, lds, bad, blockIdx.x, tn, have_tk);
+        // records (replay) keep the register prefetch: without it their
+        // tiny phase measured 3-4 % slower; table batches 5-7 % faster
+        tiny_ok = (RAMCRC_TINY_PF == 2 ? d.rec != nullptr : bool(RAMCRC_TINY_PF))
+                      ? tiny_run_cf<true>(d, so, lds, bad, blockIdx.x, tn, have_tk)
+                      : tiny_run_cf<false>(d, so, lds, bad, blockIdx.x, tn, have_tk);
         if (tiny_ok && have_tk)
             tiny_multi(d, so, lds, blockIdx.x, tn);
     }
@@ -4336,6 +4413,12 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_probe(PWalk w, uint32_t forc
         hops += __shfl_xor(hops, o, kWaveSize);
     }
     if (lane == 0) {
+        // the batch's counters, zeroed here rather than by three memsets
+        // ahead of this launch (each a few microseconds on the stream)
+        *w.n_entries = 0;
+        w.pool_used[0] = 0;
+        if (w.sum)
+            *w.sum = 0;
         uint32_t shift = kPartShift;
         if (forced) {
             shift = forced;
@@ -6219,7 +6302,6 @@ int ramcrc_replay_verify_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_
     int rc = grow_device(reinterpret_cast<void**>(&c->walk_sum), &c->walk_sum_cap, 4, sizeof(uint32_t));
     if (rc)
         return rc;
-    HIPCHK(hipMemsetAsync(c->walk_sum, 0, sizeof(uint32_t), s));
     rc = walk_impl(c, d_base, seg_stride, seg_capacity, n_seg, d_certs, d_status, d_entries,
                    entries_cap, d_n_entries, s, c->walk_sum);
     if (rc || n_seg == 0)
@@ -6241,7 +6323,12 @@ int walk_impl(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride, uint32_t s
     if ((reinterpret_cast<uintptr_t>(d_base) & 15) || (seg_stride & 15) || (seg_capacity & 15) ||
         n_seg > 0xFFFFFFFFull || (n_seg > 1 && seg_stride < seg_capacity))
         return RAMCRC_EINVAL;
-    HIPCHK(hipMemsetAsync(d_n_entries, 0, sizeof(uint64_t), s));
+    if (n_seg == 0 || c->serial_walk) {
+        // (the parallel walk's k_walk_probe zeroes these)
+        HIPCHK(hipMemsetAsync(d_n_entries, 0, sizeof(uint64_t), s));
+        if (sum)
+            HIPCHK(hipMemsetAsync(sum, 0, sizeof(uint32_t), s));
+    }
     if (n_seg == 0)
         return RAMCRC_OK;
     WalkDesc w{};
@@ -6325,7 +6412,6 @@ int walk_impl(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride, uint32_t s
         pw.pool_used = c->walk_pool_used;
         pw.pool_cap = pool_blocks;
         pw.sum = sum;
-        HIPCHK(hipMemsetAsync(c->walk_pool_used, 0, sizeof(unsigned long long), s));
         hipLaunchKernelGGL(k_walk_probe, dim3(1), dim3(kWaveSize), 0, s, pw, c->walk_pshift, geo);
         HIPCHK(hipGetLastError());
         if (nparts > 1) {
