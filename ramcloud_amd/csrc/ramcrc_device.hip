@@ -1031,6 +1031,9 @@ constexpr uint64_t kBinWgsPerCu = RAMCRC_BIN_WGS_PER_CU;   // binning grid cap p
 // -- 0 never, 1 always, 2 where the round loop has no register prefetch
 #define RAMCRC_TINY_LSEL 2
 #endif
+#ifndef RAMCRC_TINY_REGEO
+#define RAMCRC_TINY_REGEO 1   // prefetching tiny loop: window geometry re-swizzled from the owner
+#endif
 #ifndef RAMCRC_TINY_T3
 #define RAMCRC_TINY_T3 1   // tiny windows: tail masks on dword 3 only when every window ends at >= 96
 #endif
@@ -2643,7 +2646,12 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
     tiny_fill(lds);
     const TwRows rw(gl, g4);
     // without the register prefetch the selectors fit (RAMCRC_TINY_LSEL 2)
-    constexpr bool kLsel = RAMCRC_TINY_LSEL == 2 ? !kPF : bool(RAMCRC_TINY_LSEL);
+    // with the prefetch, the windows' geometry is swizzled again from the
+    // owner in the compute (RAMCRC_TINY_REGEO) so that the selectors and the
+    // second window body fit in the registers
+    constexpr bool kRegeo = kPF && RAMCRC_TINY_REGEO;
+    constexpr bool kLean = !kPF || kRegeo;
+    constexpr bool kLsel = RAMCRC_TINY_LSEL == 2 ? kLean : bool(RAMCRC_TINY_LSEL);
     TwSel ts;
     if constexpr (kLsel)
         ts = TwSel(g4);
@@ -2667,17 +2675,17 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
         }
         uint32_t mine = 0;
 #if RAMCRC_TINY_WR
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const uint32_t sa = (gc[q] >> 8) & 0xF;
-            const uint32_t e = sa + (gc[q] & 0xFF);           // window-relative end, <= 128
+        static_for8([&](auto qc) {
+            constexpr int q = decltype(qc)::value;
+            const uint32_t g = kRegeo ? swz_from<q>(o0.geo) : gc[q];
+            const uint32_t sa = (g >> 8) & 0xF;
+            const uint32_t e = sa + (g & 0xFF);           // window-relative end, <= 128
             // (a wave-uniform branch: entries of 81 B or more skip most tail masks)
-            // (not with the register prefetch: its loop has no VGPRs to spare)
-            const bool t3 = RAMCRC_TINY_T3 && !kPF && __builtin_amdgcn_ballot_w64(e < 96) == 0;
+            const bool t3 = RAMCRC_TINY_T3 && kLean && __builtin_amdgcn_ballot_w64(e < 96) == 0;
             const uint32_t R = t3 ? tiny_win_wr<kLsel, true>(lds, wc[q], sa, e, rw, gl, g4, ts)
                                   : tiny_win_wr<kLsel, false>(lds, wc[q], sa, e, rw, gl, g4, ts);
             mine = gl == uint32_t(q) ? R : mine;
-        }
+        });
 #else
 #pragma unroll
         for (int q = 0; q < 8; q++) {

@@ -9,6 +9,6 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method threa
     tests/test_gpu_binning.py tests/test_gpu_parity.py tests/test_gpu_segments.py \
     tests/test_gpu_replay_fused.py > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
-VARIANTS="${VARIANTS:-md0 pf0}" CASES="--config entries --entry-size 100;--config entries;--config replay --value-len 64;--config append" \
-    REPS=3 STEPS=20 TAG=${TAG:-r05/tinyva/ab} bash tools/gpu_ab.sh || exit 1
+VARIANTS="${VARIANTS:-md0 pf0}" CASES="${CASES:---config entries --entry-size 100;--config entries;--config replay --value-len 64;--config append}" \
+    REPS=${REPS:-3} STEPS=20 TAG=${TAG:-r05/tinyva/ab} bash tools/gpu_ab.sh || exit 1
 python tools/ab_summary.py gpurun_out/${TAG:-r05/tinyva/ab}
