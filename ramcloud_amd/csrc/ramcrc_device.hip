@@ -4395,6 +4395,15 @@ __device__ __forceinline__ PWalk walk_geo(PWalk w)
 constexpr uint32_t kPartShiftMax = 20;
 constexpr int kProbeHops = 8;
 
+// The replay summary word (PWalk::sum) goes 0 -> 1 once per batch.  A wave
+// reads it (coherently) when it starts and ORs only if it was still 0 and it
+// saw a hard record: with 1 KiB objects every wave of k_walk_copy has one,
+// and 32K same-address atomics cost 175 us per batch (21 -> 195 us).
+__device__ __forceinline__ uint32_t walk_sum_seen(const uint32_t* sum)
+{
+    return sum ? __hip_atomic_load(sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 1u;
+}
+
 __global__ __launch_bounds__(kWaveSize) void k_walk_probe(PWalk w, uint32_t forced, uint32_t* geo)
 {
     const int lane = threadIdx.x;
@@ -5456,7 +5465,7 @@ __global__ __launch_bounds__(256) void k_walk_emit(PWalk w0)
                             w.sum ? &hard : nullptr},
                   chase ? (1u << w.pshift) : pre);
     }
-    if (w.sum && __ballot(hard) && (threadIdx.x & (kWaveSize - 1)) == 0)
+    if (w.sum && __ballot(hard) && (threadIdx.x & (kWaveSize - 1)) == 0 && !walk_sum_seen(w.sum))
         atomicOr(w.sum, 1u);
 }
 
@@ -5467,6 +5476,7 @@ __global__ __launch_bounds__(256) void k_walk_emit(PWalk w0)
 // the segment's base), so a wave takes kCopyU blocks at a time and issues
 // each level's loads for all of them together.
 static_assert(kPartRec == kWaveSize, "k_walk_copy: one lane per record of a block");
+
 #ifndef RAMCRC_COPY_U
 #define RAMCRC_COPY_U 4
 #endif
@@ -5479,6 +5489,7 @@ __global__ __launch_bounds__(256) void k_walk_copy(PWalk w0)
     const uint64_t nblk = nfirst + (used < w.pool_cap ? used : w.pool_cap);
     const uint64_t nwave = uint64_t(gridDim.x) * (blockDim.x / kWaveSize);
     const uint32_t lane = threadIdx.x & (kWaveSize - 1);
+    const uint32_t seen = walk_sum_seen(w.sum);
     bool hard = false;
     for (uint64_t b0 = (uint64_t(blockIdx.x) * (blockDim.x / kWaveSize) +
                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize)) * kCopyU;
@@ -5533,11 +5544,11 @@ __global__ __launch_bounds__(256) void k_walk_copy(PWalk w0)
             const uint64_t dst = sbase[u] + r[u].rec + r[u].pre + (ri - r[u].cut);
             if (dst < w.cap) {
                 w.entries[dst] = u32x4{uint32_t(part[u] / w.nparts), v[u].x, v[u].y >> 8, v[u].y & 0xFF};
-                hard = hard || (w.sum && replay_hard(v[u].x, v[u].y >> 8, v[u].y & 0xFF));
+                hard = hard || (!seen && replay_hard(v[u].x, v[u].y >> 8, v[u].y & 0xFF));
             }
         }
     }
-    if (w.sum && __ballot(hard) && lane == 0)
+    if (!seen && __ballot(hard) && lane == 0)
         atomicOr(w.sum, 1u);
 }
 
