@@ -525,18 +525,32 @@ __device__ __forceinline__ uint64_t entry_count(const BatchDesc& d)
 }
 
 // Header bytes a record of `type` must hold to be checked; 0 = not checked.
+// (a nibble per type of bytes / 4 in one 64-bit constant: branch-free, and
+// it can never become a lookup table in memory on a per-record path)
+constexpr uint64_t replay_header_nibbles()
+{
+    const uint32_t t[][2] = {{RAMCRC_LOG_ENTRY_TYPE_OBJ, kObjHeaderBytes},
+                             {RAMCRC_LOG_ENTRY_TYPE_OBJTOMB, kTombHeaderBytes},
+                             {RAMCRC_LOG_ENTRY_TYPE_SAFEVERSION, kSafeVersionBytes},
+                             {RAMCRC_LOG_ENTRY_TYPE_PREP, kPrepHeaderBytes + kObjHeaderBytes},
+                             {RAMCRC_LOG_ENTRY_TYPE_PREPTOMB, kPrepTombBytes},
+                             {RAMCRC_LOG_ENTRY_TYPE_TXDECISION, kTxDecisionHeaderBytes},
+                             {RAMCRC_LOG_ENTRY_TYPE_TXPLIST, kTxPlistHeaderBytes}};
+    uint64_t v = 0;
+    for (const auto& e : t)
+        v |= uint64_t(e[1] / 4) << (4 * e[0]);
+    return v;
+}
+constexpr uint64_t kReplayHeaderNibbles = replay_header_nibbles();
+static_assert(kObjHeaderBytes % 4 == 0 && kTombHeaderBytes % 4 == 0 && kSafeVersionBytes % 4 == 0 &&
+                  kPrepTombBytes % 4 == 0 && kTxDecisionHeaderBytes % 4 == 0 && kTxPlistHeaderBytes % 4 == 0 &&
+                  (kPrepHeaderBytes + kObjHeaderBytes) / 4 < 16 && kTxDecisionHeaderBytes / 4 < 16 &&
+                  RAMCRC_LOG_ENTRY_TYPE_TXPLIST < 16,
+              "replay header sizes: one nibble of bytes / 4 per type below 16");
+
 __device__ __forceinline__ uint32_t replay_header_bytes(uint32_t type)
 {
-    switch (type) {
-    case RAMCRC_LOG_ENTRY_TYPE_OBJ: return kObjHeaderBytes;
-    case RAMCRC_LOG_ENTRY_TYPE_OBJTOMB: return kTombHeaderBytes;
-    case RAMCRC_LOG_ENTRY_TYPE_SAFEVERSION: return kSafeVersionBytes;
-    case RAMCRC_LOG_ENTRY_TYPE_PREP: return kPrepHeaderBytes + kObjHeaderBytes;
-    case RAMCRC_LOG_ENTRY_TYPE_PREPTOMB: return kPrepTombBytes;
-    case RAMCRC_LOG_ENTRY_TYPE_TXDECISION: return kTxDecisionHeaderBytes;
-    case RAMCRC_LOG_ENTRY_TYPE_TXPLIST: return kTxPlistHeaderBytes;
-    default: return 0;
-    }
+    return type < 16 ? 4 * uint32_t((kReplayHeaderNibbles >> (4 * type)) & 15) : 0u;
 }
 
 // The object bytes [S, E) of walk record r ({segment, offset, length,
@@ -4396,9 +4410,9 @@ constexpr uint32_t kPartShiftMax = 20;
 constexpr int kProbeHops = 8;
 
 // The replay summary word (PWalk::sum) goes 0 -> 1 once per batch.  A wave
-// reads it (coherently) when it starts and ORs only if it was still 0 and it
-// saw a hard record: with 1 KiB objects every wave of k_walk_copy has one,
-// and 32K same-address atomics cost 175 us per batch (21 -> 195 us).
+// that saw a hard record reads it (coherently) and ORs only while it is 0:
+// with 1 KiB objects every wave has one, and 32K same-address atomics cost
+// 175 us per batch when k_walk_copy made them (profiles/r05/replayfix).
 __device__ __forceinline__ uint32_t walk_sum_seen(const uint32_t* sum)
 {
     return sum ? __hip_atomic_load(sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 1u;
@@ -5489,6 +5503,10 @@ __global__ __launch_bounds__(256) void k_walk_copy(PWalk w0)
     const uint64_t nblk = nfirst + (used < w.pool_cap ? used : w.pool_cap);
     const uint64_t nwave = uint64_t(gridDim.x) * (blockDim.x / kWaveSize);
     const uint32_t lane = threadIdx.x & (kWaveSize - 1);
+    // the fused replay's summary (w.sum) over every record copied; the
+    // records C walks again set it in k_walk_emit.  (Taking it in A and the
+    // fix-up instead -- the last hard index per part, counted from each
+    // accepted part's cut -- measured 1 % slower: profiles/r05/replayfix.)
     const uint32_t seen = walk_sum_seen(w.sum);
     bool hard = false;
     for (uint64_t b0 = (uint64_t(blockIdx.x) * (blockDim.x / kWaveSize) +

@@ -1,7 +1,7 @@
 # Round 5: the replay summary read once per wave in k_walk_copy (no 32K
 # same-address atomics): GPU replay/segment tests, then the replay traces.
 set -o pipefail
-OUT=gpurun_out/r05/replayfix
+OUT=gpurun_out/r05/${TAG:-replayfix}
 mkdir -p $OUT
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
