@@ -4471,6 +4471,10 @@ __global__ __launch_bounds__(kWaveSize) void k_walk_probe(PWalk w, uint32_t forc
 constexpr uint32_t kSyncStage = RAMCRC_SYNC_STAGE_KIB * 1024;   // staged bytes per wave
 constexpr uint32_t kSyncWin = kSyncStage - 16;       // candidates / hops read from LDS below this
 constexpr int kSyncWaves = 4;                        // waves per workgroup
+#ifndef RAMCRC_SYNC_TYPES
+#define RAMCRC_SYNC_TYPES 1   // k_walk_sync: survivors whose hops are all objects / tombstones first
+#endif
+constexpr uint64_t kSyncJunkKey = 1ull << 63;        // search key bit: a survivor of the other class
 
 // Wave minimum through DPP (quad swaps, half-row and row mirrors, row
 // broadcasts): the result is valid in lane 63 and returned uniform.
@@ -4621,7 +4625,8 @@ __global__ __launch_bounds__(kSyncWaves * kWaveSize) void k_walk_sync(PWalk w0)
             const uint32_t wend = B + kSyncWin;   // peeks below wend stay in LDS
             uint64_t best = ~0ull;                // (position after two hops << 32) | candidate
             uint32_t bound = 0xFFFFFFFFu;         // nearest first hop of a survivor: h lies below it
-            for (uint32_t c0 = B; c0 < to && c0 < bound && !(RAMCRC_SYNC_EARLY && best != ~0ull);
+            // (early stop: once a survivor of the preferred class is known)
+            for (uint32_t c0 = B; c0 < to && c0 < bound && !(RAMCRC_SYNC_EARLY && best < kSyncJunkKey);
                  c0 += kSyncRound) {
                 const uint32_t cl = c0 + uint32_t(lane) * kSyncPer;
                 constexpr int kWords = (kSyncPer / 4 + 3) & ~1;
@@ -4657,6 +4662,7 @@ __global__ __launch_bounds__(kSyncWaves * kWaveSize) void k_walk_sync(PWalk w0)
                     const bool have = t0 + uint32_t(lane) < total;
                     const uint32_t c = c0 + (have ? list[t0 + uint32_t(lane)] : 0u);
                     bool live = have;
+                    bool junk = false;   // a hop whose entry is neither an object nor a tombstone
                     uint32_t p = c, first = 0, second = 0;
                     for (int hh = 0; hh < kSyncHops && __ballot(live && p < limit); hh++) {
                         if (live && p < limit) {   // (at the limit the walk ends: keep)
@@ -4670,10 +4676,14 @@ __global__ __launch_bounds__(kSyncWaves * kWaveSize) void k_walk_sync(PWalk w0)
                                 // empty entry -- junk chains through structured
                                 // object headers do both)
                                 if (plausible(q, h, w.capacity) &&
-                                    (!RAMCRC_SYNC_STRICT || (h.next <= limit && h.len != 0)))
+                                    (!RAMCRC_SYNC_STRICT || (h.next <= limit && h.len != 0))) {
                                     p = uint32_t(h.next);
-                                else
+                                    const uint32_t ty = uint32_t(q) & 0x3F;
+                                    junk = junk || (ty != RAMCRC_LOG_ENTRY_TYPE_OBJ &&
+                                                    ty != RAMCRC_LOG_ENTRY_TYPE_OBJTOMB);
+                                } else {
                                     live = false;
+                                }
                             }
                         }
                         if (hh == 0)
@@ -4687,19 +4697,29 @@ __global__ __launch_bounds__(kSyncWaves * kWaveSize) void k_walk_sync(PWalk w0)
                         first = p;
                     const uint32_t fb = wave_min(live ? first : 0xFFFFFFFFu);
                     bound = fb < bound ? fb : bound;
-                    // nearest second hop, ties to the lower candidate
-                    const uint32_t s2 = wave_min(live ? second : 0xFFFFFFFFu);
-                    if (s2 != 0xFFFFFFFFu) {
-                        const uint64_t tie = __ballot(live && second == s2);
-                        const uint32_t lo = __popcll(tie) == 1
-                                                ? uint32_t(__builtin_amdgcn_readlane(int(c), __builtin_ctzll(tie)))
-                                                : wave_min(live && second == s2 ? c : 0xFFFFFFFFu);
-                        const uint64_t key = (uint64_t(s2) << 32) | lo;
-                        best = key < best ? key : best;
+                    // nearest second hop, ties to the lower candidate; chains of
+                    // objects and tombstones first (RAMCRC_SYNC_TYPES): a fixed
+                    // object layout can hold a junk chain of another type that
+                    // runs beside the real one at the same stride and never meets
+                    // it, and then beats it on the second hop -- k_walk_fix then
+                    // re-walks the whole part (128 B values: 0.37 ms per batch)
+                    for (int cls = RAMCRC_SYNC_TYPES ? 0 : 1; cls < 2; cls++) {
+                        const bool lc = live && (cls == 1 || !junk);
+                        const uint32_t s2 = wave_min(lc ? second : 0xFFFFFFFFu);
+                        if (s2 != 0xFFFFFFFFu) {
+                            const uint64_t tie = __ballot(lc && second == s2);
+                            const uint32_t lo = __popcll(tie) == 1
+                                                    ? uint32_t(__builtin_amdgcn_readlane(int(c), __builtin_ctzll(tie)))
+                                                    : wave_min(lc && second == s2 ? c : 0xFFFFFFFFu);
+                            const uint64_t key = (RAMCRC_SYNC_TYPES && cls ? kSyncJunkKey : 0ull) |
+                                                 (uint64_t(s2) << 32) | lo;
+                            best = key < best ? key : best;
+                            break;
+                        }
                     }
                 }
             }
-            return best == ~0ull ? kNoStart : uint32_t(best);
+            return best == ~0ull ? kNoStart : uint32_t(best);   // (bit 63, the class, dropped)
         };
         // entries of up to ~2 KiB: found with LDS reads alone; longer ones
         // (their chain leaves the window) by the general search
