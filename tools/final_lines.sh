@@ -26,4 +26,5 @@ timeout -k 10 200 $P -o c3_100 -- python3 bench.py --config entries --entry-size
 timeout -k 10 200 $P -o append -- python3 bench.py --config append --steps 20 --no-cpu-baseline > "$OUT/prof_append.json" 2> "$OUT/prof_append.err" || exit 1
 timeout -k 10 300 $P -o replay -- python3 bench.py --config replay --steps 10 --no-cpu-baseline > "$OUT/prof_replay.json" 2> "$OUT/prof_replay.err" || exit 1
 timeout -k 10 300 $P -o replay64 -- python3 bench.py --config replay --value-len 64 --steps 10 --no-cpu-baseline > "$OUT/prof_replay64.json" 2> "$OUT/prof_replay64.err" || exit 1
+timeout -k 10 300 $P -o replay128 -- python3 bench.py --config replay --value-len 128 --steps 10 --no-cpu-baseline > "$OUT/prof_replay128.json" 2> "$OUT/prof_replay128.err" || exit 1
 python tools/lines_summary.py "$OUT"/*.json > "$OUT/lines.txt" 2>&1
