@@ -1045,6 +1045,9 @@ constexpr uint64_t kBinWgsPerCu = RAMCRC_BIN_WGS_PER_CU;   // binning grid cap p
 // -- 0 never, 1 always, 2 where the round loop has no register prefetch
 #define RAMCRC_TINY_LSEL 2
 #endif
+#ifndef RAMCRC_TINY_M2
+#define RAMCRC_TINY_M2 1   // tiny_multi: bin 2 with two-window buffers and a ring of four
+#endif
 #ifndef RAMCRC_TINY_REGEO
 #define RAMCRC_TINY_REGEO 1   // prefetching tiny loop: window geometry re-swizzled from the owner
 #endif
@@ -2796,13 +2799,18 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
 }
 
 // bins 2 .. kTinyK (see above): one entry per q as in tiny_run_cf, all K
-// windows of the group's next entry loaded while the current one is hashed
-// (two buffers of kTinyK windows instead of a round of first windows).
-__device__ __forceinline__ void tiny_multi(const BatchDesc& d, const Sorted& so, const uint8_t* lds,
-                                           uint32_t blk, uint32_t nblk)
+// windows of a group's entry loaded while earlier ones are hashed: a ring of
+// kDepth buffers of kK windows, the entry kDepth - 1 ahead loaded at each q.
+// Bin 2 (entries of at most two windows: the objects of 128-byte values) runs
+// with kK = 2 and a ring of 4 -- three entries in flight per group for the
+// registers the general loop spends on two buffers of four windows; bins 3 ..
+// kTinyK with kK = kTinyK and two buffers.
+template <int kK, int kDepth>
+__device__ __forceinline__ void tiny_multi_run(const BatchDesc& d, const Sorted& so, const uint8_t* lds,
+                                               uint32_t blk, uint32_t nblk, uint64_t s0, uint64_t s1)
 {
-    const uint64_t s0 = so.bt->start[2], s1 = so.bt->start[kTinyK + 1];
-    if (kTinyK < 2 || s0 == s1)
+    static_assert(kDepth >= 2 && 8 % kDepth == 0, "tiny_multi: ring index q % kDepth must be static");
+    if (s0 == s1)
         return;   // uniform
     const int lane = threadIdx.x & (kWaveSize - 1);
     const uint32_t gl = uint32_t(lane) & 7;
@@ -2855,13 +2863,13 @@ __device__ __forceinline__ void tiny_multi(const BatchDesc& d, const Sorted& so,
     const TwRows rw(gl, g4);
     // the windows of the entry (geo, S) into w: window k is [A + 128 k, + 128);
     // a dword at or past the window's last entry byte reads that byte's dword
-    auto load_entry = [&](uint32_t geo, uint64_t S, u32x4 (&w)[kTinyK]) {
+    auto load_entry = [&](uint32_t geo, uint64_t S, u32x4 (&w)[kK]) {
         const uint32_t K = tk_windows(geo);
         const uint32_t el = (geo & 0x3FF) - tk_tail(geo) - 128 * (K - 1);   // last window's end
 #if RAMCRC_TINY_LD16
         const uint64_t A = S & ~uint64_t(15);
 #pragma unroll
-        for (int k = 0; k < kTinyK; k++) {
+        for (int k = 0; k < kK; k++) {
             if (uint32_t(k) < K) {
                 const uint32_t e = uint32_t(k) + 1 == K ? el : 128u;
                 const uint32_t pl = (max(int(e) - 1, 0) & ~15);
@@ -2871,7 +2879,7 @@ __device__ __forceinline__ void tiny_multi(const BatchDesc& d, const Sorted& so,
 #else
         const uint64_t au = (S & ~uint64_t(15)) + 4 * gl;
 #pragma unroll
-        for (int k = 0; k < kTinyK; k++) {
+        for (int k = 0; k < kK; k++) {
             if (uint32_t(k) < K) {
                 const uint32_t e = uint32_t(k) + 1 == K ? el : 128u;
                 const int lim = (max(int(e) - 1, 0) & ~3) - int(4 * gl);
@@ -2884,17 +2892,29 @@ __device__ __forceinline__ void tiny_multi(const BatchDesc& d, const Sorted& so,
         }
 #endif
     };
+    // entry qe of the round whose owners are `on` (swizzled from lane 8g + qe)
+    auto load_q = [&](auto qc, const TinyCf& on, bool valid, uint32_t& gq, u32x4 (&w)[kK]) {
+        constexpr int qe = decltype(qc)::value;
+        uint32_t g = swz_from<qe>(on.geo);
+        g = valid ? g : 0u;
+        const uint64_t Sn = (uint64_t(swz_from<qe>(uint32_t(on.S >> 32))) << 32) | swz_from<qe>(uint32_t(on.S));
+        gq = g;
+        load_entry(g, Sn, w);
+    };
 
     uint64_t r = wave;
     TinyRaw w1 = load_raw(r + nwaves);
     TinyCf o0 = own_of(load_raw(r));
     uint32_t sc, tc;
     own_loads(o0, sc, tc);
-    u32x4 buf[2][kTinyK];
-    uint32_t gq[2];
-    gq[0] = swz_from<0>(o0.geo);
-    load_entry(gq[0], (uint64_t(swz_from<0>(uint32_t(o0.S >> 32))) << 32) | swz_from<0>(uint32_t(o0.S)),
-               buf[0]);
+    u32x4 buf[kDepth][kK];
+    uint32_t gq[kDepth];
+    // the ring's first kDepth - 1 entries
+    static_for8([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if constexpr (j < kDepth - 1)
+            load_q(jc, o0, true, gq[j], buf[j]);
+    });
     for (; r < rounds; r += nwaves) {
         const TinyRaw w2 = load_raw(r + 2 * nwaves);
         const TinyCf o1 = own_of(w1);   // loaded a round ago
@@ -2904,29 +2924,28 @@ __device__ __forceinline__ void tiny_multi(const BatchDesc& d, const Sorted& so,
         uint32_t mine = 0;
         static_for8([&](auto qc) {
             constexpr int q = decltype(qc)::value;
-            // the group's next entry: q + 1 of this round, or q 0 of the next
+            // the group's entry kDepth - 1 ahead: of this round, or of the next
             {
-                constexpr int qn = (q + 1) & 7;
-                const TinyCf& on = q < 7 ? o0 : o1;
-                uint32_t g = swz_from<qn>(on.geo);
-                g = q < 7 || more ? g : 0u;
-                const uint64_t Sn = (uint64_t(swz_from<qn>(uint32_t(on.S >> 32))) << 32) |
-                                    swz_from<qn>(uint32_t(on.S));
-                gq[(q + 1) & 1] = g;
-                load_entry(g, Sn, buf[(q + 1) & 1]);
+                constexpr int qn = q + kDepth - 1;
+                constexpr int bn = qn % kDepth;
+                if constexpr (qn < 8)
+                    load_q(std::integral_constant<int, qn>{}, o0, true, gq[bn], buf[bn]);
+                else
+                    load_q(std::integral_constant<int, qn - 8>{}, o1, more, gq[bn], buf[bn]);
             }
-            const uint32_t geo = gq[q & 1];
+            constexpr int bq = q % kDepth;
+            const uint32_t geo = gq[bq];
             const uint32_t K = tk_windows(geo);
             const uint32_t el = (geo & 0x3FF) - tk_tail(geo) - 128 * (K - 1);
             // window sums at their distance from their window's end; Horner with
             // X^128 between windows: acc is relative to the last window's end
-            uint32_t acc = tiny_win_wr(lds, buf[q & 1][0], (geo >> 10) & 0xF,
+            uint32_t acc = tiny_win_wr(lds, buf[bq][0], (geo >> 10) & 0xF,
                                        K > 1 ? 128u : (K ? el : 0u), rw, gl, g4);
 #pragma unroll
-            for (int k = 1; k < kTinyK; k++) {
+            for (int k = 1; k < kK; k++) {
                 if (__builtin_amdgcn_ballot_w64(uint32_t(k) < K)) {   // uniform
                     const uint32_t e = uint32_t(k) + 1 == K ? el : 128u;
-                    const uint32_t R = tiny_win_wr(lds, buf[q & 1][k], 0, uint32_t(k) < K ? e : 0u, rw, gl, g4);
+                    const uint32_t R = tiny_win_wr(lds, buf[bq][k], 0, uint32_t(k) < K ? e : 0u, rw, gl, g4);
                     // X^128(acc) by lanes gl & 3 (byte gl & 3 at distance 128 - (gl & 3))
                     const uint32_t kk = gl & 3;
                     uint32_t X = *reinterpret_cast<const uint32_t*>(lds + tw_addr(kk, (acc >> (8 * kk)) & 0xFF));
@@ -2963,6 +2982,23 @@ __device__ __forceinline__ void tiny_multi(const BatchDesc& d, const Sorted& so,
         w1 = w2;
         sc = sn;
         tc = tn;
+    }
+}
+
+__device__ __forceinline__ void tiny_multi(const BatchDesc& d, const Sorted& so, const uint8_t* lds,
+                                           uint32_t blk, uint32_t nblk)
+{
+    if constexpr (kTinyK >= 2) {
+        const uint64_t s0 = so.bt->start[2], s1 = so.bt->start[kTinyK + 1];
+        if (s0 == s1)
+            return;   // uniform
+        if constexpr (RAMCRC_TINY_M2 && kTinyK > 2) {
+            const uint64_t s2 = so.bt->start[3];
+            tiny_multi_run<2, 4>(d, so, lds, blk, nblk, s0, s2);
+            tiny_multi_run<kTinyK, 2>(d, so, lds, blk, nblk, s2, s1);
+        } else {
+            tiny_multi_run<kTinyK, 2>(d, so, lds, blk, nblk, s0, s1);
+        }
     }
 }
 
