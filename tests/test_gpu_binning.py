@@ -181,6 +181,30 @@ def test_all_tiny_batch_direct_path(ctx, ramcrc, oracle_mod, api):
 
 
 @pytest.mark.parametrize("api", ["entries", "batch"])
+def test_direct_path_long_windows(ctx, ramcrc, oracle_mod, api):
+    """All-tiny batches whose windows mostly end at >= 96 bytes, where the
+    tiny loop skips the tail masks of dwords 0-2 (RAMCRC_TINY_T3, a ballot
+    per q): entries of 81-112 bytes at every alignment, then 60-112 bytes so
+    that waves mix the masked and unmasked window bodies, with and without
+    initial states."""
+    rng = np.random.default_rng(8196)
+    host = oracle_mod.splitmix_bytes(41, 1 << 20)
+    base = dev(host)
+    n = 50000
+    offs = rng.integers(0, (1 << 20) - 4000, n)
+    for lo in (81, 60):
+        lens = rng.integers(lo, 113, n)
+        lens = np.minimum(lens, 128 - (offs % 16))   # one window each: E - (S & ~15) <= 128
+        init = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+        for it in (None, init):
+            got = host_u32(run(ctx, api, base, offs, lens, it))
+            want = oracle_mod.entries(host, offs, lens, init=it)
+            bad = np.nonzero(got != want)[0]
+            assert bad.size == 0, [(int(offs[i]) % 16, int(lens[i])) for i in bad[:8]]
+    ctx.check()
+
+
+@pytest.mark.parametrize("api", ["entries", "batch"])
 def test_one_launch_threshold(ctx, oracle_mod, api):
     """Batches either side of the one-launch binning limit (one 4,096-entry
     tile per 1,024-thread workgroup, one workgroup per CU -- half of the two a
