@@ -166,13 +166,16 @@ def test_walk_small_records_default_table_no_check(ramcrc, oracle_mod):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("value_len", [64, 1024, 8192, 100000])
+@pytest.mark.parametrize("value_len", [64, 128, 256, 1024, 8192, 100000])
 def test_parallel_walk_8mib_vs_oracle(ramcrc, oracle_mod, value_len):
     """8 MiB object segments (128 parts of the parallel walk) at the
     RecoverSegmentBenchmark value sizes: entries from 101 B to larger than a
-    part; one segment with a damaged length in its middle (the chain derails:
-    every later part misguessed) and one with a wrong certificate.  Status,
-    records and object CRCs equal the oracle's and the serial walker's."""
+    part (128 B values: objects of two windows, the multi-window tiny phase's
+    ring, and a layout that holds a same-stride junk chain; 256 B: three
+    windows); one segment with a damaged length in its middle (the chain
+    derails: every later part misguessed) and one with a wrong certificate.
+    Status, records and object CRCs equal the oracle's and the serial
+    walker's."""
     import torch
     cap, nseg = 8 << 20, 6
     buf, certs, counts = segments.object_segments_host(nseg, cap, value_len, threads=8)
