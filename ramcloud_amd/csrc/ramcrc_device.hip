@@ -971,6 +971,9 @@ constexpr int kPU = RAMCRC_PU;             // ping-pong depth (pipelined bins)
 #ifndef RAMCRC_TINY_SAFE
 #define RAMCRC_TINY_SAFE 1    // tiny_run_cf: unclamped window loads when every window of a q is page-safe
 #endif
+#ifndef RAMCRC_TINY_OVL
+#define RAMCRC_TINY_OVL 1   // tiny phase: round 0's windows in flight while the table is built
+#endif
 #ifndef RAMCRC_TINY_EARLY
 #define RAMCRC_TINY_EARLY 0   // tiny phase: round 0's window loads issued before the table fill
 #endif
@@ -2326,21 +2329,35 @@ __device__ __forceinline__ void tiny_fill_wr(uint8_t* lds)
 // 64 rows land on 32 banks).  Threads 0 .. 31 then build X^-128 the same way.
 // The copy it replaces moved 132 KiB per CU through the L2 (33 MB per launch
 // over the chip; 4.3 us of a 35 us 1M x 100 B launch, profiles/r04/ab).
-__device__ __forceinline__ void tiny_fill_gen(uint8_t* lds)
+// (split in two so that a caller can put loads of its own between them: the
+// basis words' loads, then the build once they have landed)
+struct TinyBasis {
+    uint4 lo, hi, a, c;
+};
+
+__device__ __forceinline__ TinyBasis tiny_basis_load()
+{
+    TinyBasis t;
+    const uint32_t q = threadIdx.x & 127;
+    const uint4* bp = reinterpret_cast<const uint4*>(g_tab.twb[q]);
+    t.lo = bp[0];
+    t.hi = bp[1];
+    t.a = t.c = make_uint4(0u, 0u, 0u, 0u);
+    if (threadIdx.x < 32) {   // X^-128: table j = t / 8, columns 32 (t % 8) ..
+        const uint4* ip = reinterpret_cast<const uint4*>(g_tab.twib[threadIdx.x >> 3]);
+        t.a = ip[0];
+        t.c = ip[1];
+    }
+    return t;
+}
+
+__device__ __forceinline__ void tiny_fill_build(uint8_t* lds, const TinyBasis& tb)
 {
     static_assert(kEntWaves * kWaveSize == 1024, "one (row, column block) per thread");
     const uint32_t q = threadIdx.x & 127, b0 = 32 * (threadIdx.x >> 7);
-    const uint4* bp = reinterpret_cast<const uint4*>(g_tab.twb[q]);
-    const uint4 lo = bp[0], hi = bp[1];
-    const uint32_t B[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-    uint32_t iv[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    const bool inv = threadIdx.x < 32;   // X^-128: table j = t / 8, columns 32 (t % 8) ..
-    if (inv) {
-        const uint4* ip = reinterpret_cast<const uint4*>(g_tab.twib[threadIdx.x >> 3]);
-        const uint4 a = ip[0], c = ip[1];
-        iv[0] = a.x; iv[1] = a.y; iv[2] = a.z; iv[3] = a.w;
-        iv[4] = c.x; iv[5] = c.y; iv[6] = c.z; iv[7] = c.w;
-    }
+    const uint32_t B[8] = {tb.lo.x, tb.lo.y, tb.lo.z, tb.lo.w, tb.hi.x, tb.hi.y, tb.hi.z, tb.hi.w};
+    const uint32_t iv[8] = {tb.a.x, tb.a.y, tb.a.z, tb.a.w, tb.c.x, tb.c.y, tb.c.z, tb.c.w};
+    const bool inv = threadIdx.x < 32;
     uint32_t T[32];
     T[0] = ((b0 >> 5) & 1 ? B[5] : 0u) ^ ((b0 >> 6) & 1 ? B[6] : 0u) ^ ((b0 >> 7) & 1 ? B[7] : 0u);
 #pragma unroll
@@ -2362,6 +2379,11 @@ __device__ __forceinline__ void tiny_fill_gen(uint8_t* lds)
         for (int i = 0; i < 32; i++)
             dst[i] = U[i];
     }
+}
+
+__device__ __forceinline__ void tiny_fill_gen(uint8_t* lds)
+{
+    tiny_fill_build(lds, tiny_basis_load());
 }
 #endif
 
@@ -2650,6 +2672,16 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
     };
 #endif
 
+    // RAMCRC_TINY_OVL: the table's basis words are loaded first, round 0's
+    // windows issued as soon as its owners are known, and the table built
+    // while those loads are in flight (the build waits for the basis alone)
+    constexpr bool kOvl = RAMCRC_TINY_OVL && RAMCRC_TINY_GEN && RAMCRC_TINY_WR && !RAMCRC_TINY_LD16 &&
+                          !RAMCRC_TINY_EARLY;
+#if RAMCRC_TINY_GEN && !RAMCRC_TINY_LD16
+    TinyBasis tb;
+    if constexpr (kOvl)
+        tb = tiny_basis_load();
+#endif
     uint64_t r = wave;
     TinyOwn o0 = load_own(r), o1 = load_own(r + nwaves);
     u32x4 wc[8];
@@ -2660,7 +2692,16 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
     issue(o0, wc, gc, sc);
 #endif
 #if RAMCRC_TINY_WR
+#if RAMCRC_TINY_GEN && !RAMCRC_TINY_LD16
+    if constexpr (kOvl) {
+        issue(o0, wc, gc, sc);
+        tiny_fill_build(lds, tb);
+    } else {
+        tiny_fill(lds);
+    }
+#else
     tiny_fill(lds);
+#endif
     const TwRows rw(gl, g4);
     // without the register prefetch the selectors fit (RAMCRC_TINY_LSEL 2)
     // with the prefetch, the windows' geometry is swizzled again from the
@@ -2680,7 +2721,8 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
     RAMCRC_STAMP(5);
     bool first_round = true;
 #if !RAMCRC_TINY_EARLY
-    issue(o0, wc, gc, sc);
+    if constexpr (!kOvl)
+        issue(o0, wc, gc, sc);
 #endif
     for (; r < rounds; r += nwaves) {
         const TinyOwn o2 = load_own(r + 2 * nwaves);
