@@ -974,15 +974,6 @@ constexpr int kPU = RAMCRC_PU;             // ping-pong depth (pipelined bins)
 #ifndef RAMCRC_TINY_OVL
 #define RAMCRC_TINY_OVL 1   // tiny phase: round 0's windows in flight while the table is built
 #endif
-#ifndef RAMCRC_TINY_EARLY
-#define RAMCRC_TINY_EARLY 0   // tiny phase: round 0's window loads issued before the table fill
-#endif
-#ifndef RAMCRC_TINY_LD16
-#define RAMCRC_TINY_LD16 0   // tiny phases: one 16-byte load per lane per window (layout above)
-#endif
-#ifndef RAMCRC_TINY_LD4
-#define RAMCRC_TINY_LD4 0   // A/B only: tiny windows as one 16-byte load per lane, wrong CRCs
-#endif
 #ifndef RAMCRC_TINY_PROBE
 #define RAMCRC_TINY_PROBE 0  // A/B only: conflict-free lookup addresses, wrong CRCs
 #endif
@@ -2238,57 +2229,11 @@ constexpr uint32_t kTwInvOff = 131072;
 constexpr uint32_t kLdsTinyWr = kTwInvOff + 4096;
 static_assert(kLdsTinyWr <= kLdsEntries, "k_entries' LDS holds the tiny phases' tables");
 
-#if RAMCRC_TINY_LD16
-// RAMCRC_TINY_LD16: position q = 4 r + k at ((k >> 1) << 16) | (b << 8) |
-// ((k & 1) << 7) | (r << 2) -- byte k of every dword in a plane of its own
-// (two planes share a 256-byte column), so a lane's 16 contiguous bytes (one
-// load) map to rows r = o / 4 of their dwords, and the banks stay distinct by
-// rotating each group's dword order (below).
-__device__ __forceinline__ uint32_t tw_addr(uint32_t q, uint32_t b)
-{
-    return (((q & 3) >> 1) << 16) | (b << 8) | ((q & 1) << 7) | ((q >> 2) << 2);
-}
-#else
 __device__ __forceinline__ uint32_t tw_addr(uint32_t q, uint32_t b)
 {
     return ((q >> 6) << 16) | (b << 8) | ((q & 63) << 2);
 }
-#endif
 
-#if RAMCRC_TINY_LD16
-__device__ __forceinline__ void tiny_fill_wr(uint8_t* lds)
-{
-    // plane kk, column b, row r (r = q >> 2): X^(128 - q)(b), q = 4 r + kk, from
-    // g_tab.post word 128 (255 - b) + q; one 16-byte LDS chunk = rows 4 c .. 4 c + 3
-    // at tw_addr(16 c + kk, b)
-    constexpr uint32_t kChunks = 4 * 256 * 8, kAll = kChunks + 256;
-    constexpr uint32_t kPer = (kAll + kEntWaves * kWaveSize - 1) / (kEntWaves * kWaveSize);
-    const uint32_t* post = g_tab.post;
-    const uint4* inv = reinterpret_cast<const uint4*>(&g_tab.xinv128);
-    uint4 v[kPer];
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; j++) {
-        const uint32_t i = threadIdx.x + j * (kEntWaves * kWaveSize);
-        if (i < kChunks) {
-            const uint32_t kk = i >> 11, b = (i >> 3) & 255, c = i & 7;
-            const uint32_t* w = post + 128 * (255 - b) + 16 * c + kk;
-            v[j] = make_uint4(w[0], w[4], w[8], w[12]);
-        } else if (i < kAll) {
-            v[j] = inv[i - kChunks];
-        }
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; j++) {
-        const uint32_t i = threadIdx.x + j * (kEntWaves * kWaveSize);
-        if (i < kChunks) {
-            const uint32_t kk = i >> 11, b = (i >> 3) & 255, c = i & 7;
-            *reinterpret_cast<uint4*>(lds + tw_addr(16 * c + kk, b)) = v[j];
-        } else if (i < kAll) {
-            *reinterpret_cast<uint4*>(lds + kTwInvOff + 16 * (i - kChunks)) = v[j];
-        }
-    }
-}
-#else
 __device__ __forceinline__ void tiny_fill_wr(uint8_t* lds)
 {
     // 8192 chunks of 16 B, chunk (h, b, c) = words 128 (255 - b) + 64 h + 4 c .. of
@@ -2315,12 +2260,11 @@ __device__ __forceinline__ void tiny_fill_wr(uint8_t* lds)
             *reinterpret_cast<uint4*>(lds + 16 * i) = v[j];
     }
 }
-#endif
 
 #ifndef RAMCRC_TINY_GEN
 #define RAMCRC_TINY_GEN 1   // tiny tables built in LDS from 8 basis words per row (0: copied from g_tab)
 #endif
-#if RAMCRC_TINY_GEN && !RAMCRC_TINY_LD16
+#if RAMCRC_TINY_GEN
 // The tiny phases' tables built in place instead of copied: X^m is linear, so
 // row q of X^(128 - q)(b) is the XOR of the basis words twb[q][k] over the set
 // bits k of b.  Thread t takes row q = t % 128 and the 32 columns b0 .. b0 + 31,
@@ -2389,24 +2333,6 @@ __device__ __forceinline__ void tiny_fill_gen(uint8_t* lds)
 
 // Per-lane address constants: byte k of a rotated dword (window position
 // 32 j + 4 u + ((k + g4) & 3)) of dword pair j >> 1; + 128 for odd j.
-#if RAMCRC_TINY_LD16
-// Lane u holds window bytes 16 u .. 16 u + 15 (one 16-byte load); at
-// instruction j it takes its dword (j + g4) & 3 -- window offset o = 16 u +
-// 4 ((j + g4) & 3) -- so the 32 lanes of a half-wave read 32 distinct rows
-// (banks).  P[j] = {o, o | 128, 1, 0}: one v_perm forms the address of byte
-// k of the dword (tw_addr(o + k, data byte)) from P[j] and the data.
-struct TwRows {
-    uint32_t P[4];
-    __device__ TwRows(uint32_t gl, uint32_t g4)
-    {
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t o = 16 * gl + 4 * ((uint32_t(j) + g4) & 3);
-            P[j] = 0x00010000u | ((o | 128u) << 8) | o;
-        }
-    }
-};
-#else
 struct TwRows {
     uint32_t lr[2][4];
     __device__ TwRows(uint32_t gl, uint32_t g4)
@@ -2418,7 +2344,6 @@ struct TwRows {
                 lr[h][k] = (uint32_t(h) << 16) | (16 * gl + 4 * ((uint32_t(k) + g4) & 3));
     }
 };
-#endif
 
 // Per-lane v_perm selectors for tiny_win_wr<true>: lookup k of a dword takes
 // its byte (k + g4) & 3 straight into address bits 8-15, which replaces the
@@ -2436,41 +2361,6 @@ struct TwSel {
 
 // The group's sum over one window's bytes in [sa, e), byte b at position o
 // as X^(128 - o)(b) (relative to the window's end; all 8 lanes get it).
-#if RAMCRC_TINY_LD16
-template <bool kLsel = false, bool kTail3 = false>
-__device__ __forceinline__ uint32_t tiny_win_wr(const uint8_t* lds, const u32x4& wv, uint32_t sa,
-                                                uint32_t e, const TwRows& rw, uint32_t gl, uint32_t g4,
-                                                const TwSel& = TwSel())
-{
-    // this group's dword order: instruction j takes dword (j + g4) & 3
-    const uint32_t w0 = wv.x, w1 = wv.y, w2 = wv.z, w3 = wv.w;
-    const bool b0 = g4 & 1, b1 = g4 & 2;
-    const uint32_t t0 = b0 ? w1 : w0, t1 = b0 ? w2 : w1, t2 = b0 ? w3 : w2, t3 = b0 ? w0 : w3;
-    const uint32_t ws[4] = {b1 ? t2 : t0, b1 ? t3 : t1, b1 ? t0 : t2, b1 ? t1 : t3};
-    uint32_t v[16];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int o = int(rw.P[j] & 0xFF);   // the dword's window offset
-        // bytes of [sa, e): clamp(e - o, 0, 4) from the bottom, none below sa
-        const uint32_t sh = uint32_t(min(max(32 - 8 * (int(e) - o), 0), 32));
-        const uint32_t hd = uint32_t(min(max(8 * (int(sa) - o), 0), 32));
-        const uint32_t keep = uint32_t(uint64_t(0xFFFFFFFFu) >> sh) & uint32_t(~uint64_t(0) << hd);
-        const uint32_t x = ws[j] & keep;
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-            v[4 * j + k] = *reinterpret_cast<const uint32_t*>(
-                lds + __builtin_amdgcn_perm(x, rw.P[j],
-                                            0x0C000000u | ((k >> 1) ? 0x00020000u : 0x000C0000u) |
-                                                ((4u + uint32_t(k)) << 8) | uint32_t(k & 1)));
-    }
-    const uint32_t a0 = xor3(v[0], v[1], v[2]), a1 = xor3(v[3], v[4], v[5]);
-    const uint32_t a2 = xor3(v[6], v[7], v[8]), a3 = xor3(v[9], v[10], v[11]);
-    const uint32_t a4 = xor3(v[12], v[13], v[14]);
-    uint32_t R = xor3(xor3(a0, a1, a2), xor3(a3, a4, v[15]), 0u);
-    R = group8_xor_all(R);
-    return R;
-}
-#else
 // kTail3: the caller knows e >= 96 for every window of the wave, so dwords
 // 0-2 (window offsets below 96) need no tail mask
 template <bool kLsel = false, bool kTail3 = false>
@@ -2523,11 +2413,10 @@ __device__ __forceinline__ uint32_t tiny_win_wr(const uint8_t* lds, const u32x4&
     R = group8_xor_all(R);
     return R;
 }
-#endif
 
 __device__ __forceinline__ void tiny_fill(uint8_t* lds)
 {
-#if RAMCRC_TINY_GEN && !RAMCRC_TINY_LD16
+#if RAMCRC_TINY_GEN
     tiny_fill_gen(lds);
 #else
     tiny_fill_wr(lds);
@@ -2640,27 +2529,17 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
             u32x4 v;
             if (RAMCRC_TINY_SAFE && __builtin_amdgcn_ballot_w64(!((geo[q] >> 12) & 1)) == 0) {
                 // every window of this q is page-safe: plain loads, immediate offsets
-#if RAMCRC_TINY_LD4 || RAMCRC_TINY_LD16
-                v = load16(A + 16 * gl);   // (LD4: an A/B probe with the old layout, wrong CRCs)
-#else
                 v.x = *reinterpret_cast<g32*>(au);
                 v.y = *reinterpret_cast<g32*>(au + 32);
                 v.z = *reinterpret_cast<g32*>(au + 64);
                 v.w = *reinterpret_cast<g32*>(au + 96);
-#endif
             } else {
                 const uint32_t e = ((geo[q] >> 8) & 0xF) + (geo[q] & 0xFF);   // E - A (0: empty)
-#if RAMCRC_TINY_LD16
-                // a piece at or past the entry's last byte reads that byte's piece
-                const uint32_t pl = (max(int(e) - 1, 0) & ~15);
-                v = load16(A + (16 * gl < pl ? 16 * gl : pl));
-#else
                 const int el = (max(int(e) - 1, 0) & ~3) - int(4 * gl);   // last dword, from 4 u
                 v.x = *reinterpret_cast<g32*>(au + min(0, el));
                 v.y = *reinterpret_cast<g32*>(au + min(32, el));
                 v.z = *reinterpret_cast<g32*>(au + min(64, el));
                 v.w = *reinterpret_cast<g32*>(au + min(96, el));
-#endif
             }
             w[q] = v;
         });
@@ -2675,9 +2554,8 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
     // RAMCRC_TINY_OVL: the table's basis words are loaded first, round 0's
     // windows issued as soon as its owners are known, and the table built
     // while those loads are in flight (the build waits for the basis alone)
-    constexpr bool kOvl = RAMCRC_TINY_OVL && RAMCRC_TINY_GEN && RAMCRC_TINY_WR && !RAMCRC_TINY_LD16 &&
-                          !RAMCRC_TINY_EARLY;
-#if RAMCRC_TINY_GEN && !RAMCRC_TINY_LD16
+    constexpr bool kOvl = RAMCRC_TINY_OVL && RAMCRC_TINY_GEN && RAMCRC_TINY_WR;
+#if RAMCRC_TINY_GEN
     TinyBasis tb;
     if constexpr (kOvl)
         tb = tiny_basis_load();
@@ -2686,13 +2564,8 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
     TinyOwn o0 = load_own(r), o1 = load_own(r + nwaves);
     u32x4 wc[8];
     uint32_t gc[8], sc;
-#if RAMCRC_TINY_EARLY
-    // round 0's windows in flight while the table is filled (the fill's own
-    // loads are issued after them, so their waits cover both: max, not sum)
-    issue(o0, wc, gc, sc);
-#endif
 #if RAMCRC_TINY_WR
-#if RAMCRC_TINY_GEN && !RAMCRC_TINY_LD16
+#if RAMCRC_TINY_GEN
     if constexpr (kOvl) {
         issue(o0, wc, gc, sc);
         tiny_fill_build(lds, tb);
@@ -2720,10 +2593,8 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
         return false;
     RAMCRC_STAMP(5);
     bool first_round = true;
-#if !RAMCRC_TINY_EARLY
     if constexpr (!kOvl)
         issue(o0, wc, gc, sc);
-#endif
     for (; r < rounds; r += nwaves) {
         const TinyOwn o2 = load_own(r + 2 * nwaves);
         u32x4 wn[8];
@@ -2908,17 +2779,6 @@ __device__ __forceinline__ void tiny_multi_run(const BatchDesc& d, const Sorted&
     auto load_entry = [&](uint32_t geo, uint64_t S, u32x4 (&w)[kK]) {
         const uint32_t K = tk_windows(geo);
         const uint32_t el = (geo & 0x3FF) - tk_tail(geo) - 128 * (K - 1);   // last window's end
-#if RAMCRC_TINY_LD16
-        const uint64_t A = S & ~uint64_t(15);
-#pragma unroll
-        for (int k = 0; k < kK; k++) {
-            if (uint32_t(k) < K) {
-                const uint32_t e = uint32_t(k) + 1 == K ? el : 128u;
-                const uint32_t pl = (max(int(e) - 1, 0) & ~15);
-                w[k] = load16(A + 128 * uint64_t(k) + (16 * gl < pl ? 16 * gl : pl));
-            }
-        }
-#else
         const uint64_t au = (S & ~uint64_t(15)) + 4 * gl;
 #pragma unroll
         for (int k = 0; k < kK; k++) {
@@ -2932,7 +2792,6 @@ __device__ __forceinline__ void tiny_multi_run(const BatchDesc& d, const Sorted&
                 w[k].w = *reinterpret_cast<g32*>(aw + min(96, lim));
             }
         }
-#endif
     };
     // entry qe of the round whose owners are `on` (swizzled from lane 8g + qe)
     auto load_q = [&](auto qc, const TinyCf& on, bool valid, uint32_t& gq, u32x4 (&w)[kK]) {
