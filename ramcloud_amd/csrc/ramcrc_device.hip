@@ -947,14 +947,10 @@ constexpr int kSmallK = RAMCRC_SMALLK;     // bins 2..kSmallK: octets loaded one
 #ifndef RAMCRC_TINY_K
 #define RAMCRC_TINY_K 4
 #endif
-#ifndef RAMCRC_TINY_WR
-#define RAMCRC_TINY_WR 1   // tiny phases: window-relative table, one v_perm per address, owner un-shift
-#endif
 // bins 2 .. kTinyK (entries of 2 .. kTinyK windows, e.g. objects of 129 ..
 // ~500 B): the multi-window tiny phase (tiny_run_cf<true>); 1 = off (the short bins)
 constexpr int kTinyK = RAMCRC_TINY_K;
 static_assert(kTinyK >= 1 && kTinyK <= 7, "tiny windows: E - A (<= 128 kTinyK) fits 10 bits");
-static_assert(kTinyK == 1 || RAMCRC_TINY_WR, "tiny_multi uses the window-relative table");
 #ifndef RAMCRC_ENT_NT
 #define RAMCRC_ENT_NT 1
 #endif
@@ -1973,159 +1969,6 @@ __device__ __forceinline__ void static_for8(F&& f)
     }
 }
 
-// The first phase of k_entries; lds holds the position table (kLdsTiny bytes).
-// Returns false (uniformly) when `bad` is set in any thread of the block: the
-// bin layout disagrees with the scatter, and no slot has been dereferenced.
-__device__ __forceinline__ bool tiny_run(const BatchDesc& d, const Sorted& so, uint8_t* lds,
-                                         bool bad, uint32_t blk, uint32_t nblk)
-{
-    if (so.bt->start[2] == so.bt->start[0])
-        return true;   // no entry of at most one window (uniform: every wave exits)
-    const int lane = threadIdx.x & (kWaveSize - 1);
-    const int gl = lane & 7;
-    const uint64_t wave = uint64_t(blk) * kEntWaves +
-                          __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize);
-    const uint64_t nwaves = uint64_t(nblk) * kEntWaves;
-    const uint64_t s0 = so.bt->start[0], s1 = so.bt->start[2];
-    const uint64_t rounds = (s1 - s0 + 63) / 64;
-    const bool finalize = d.flags & RAMCRC_FINALIZE;
-    const uint64_t dummy = reinterpret_cast<uint64_t>(so.bt);
-
-    auto load_own = [&](uint64_t r) -> TinyOwn {
-        TinyOwn o;
-        const uint64_t sl = s0 + r * 64 + uint32_t(lane);
-        u32x4 dd = {0u, 0u, 0u, 0u};
-        o.ix = kNoIdx;
-        o.init = 0xFFFFFFFFu;
-        if (r < rounds && sl < s1) {
-            dd = so.desc[sl];
-            o.ix = so.idx[sl];
-            if (d.init)
-                o.init = so.init[sl];
-        }
-        o.S = (uint64_t(dd.y) << 32) | dd.x;
-        const uint64_t E = (uint64_t(dd.w) << 32) | dd.z;
-        o.len = uint32_t(E - o.S);
-        o.A = o.S & ~uint64_t(15);
-        o.geo = (o.ix != kNoIdx && o.len >= 4) ? (o.len | (uint32_t(o.S - o.A) << 8)) : 0u;
-        return o;
-    };
-    // the group's eight windows: piece gl of each owner's 128-byte window
-    auto issue = [&](const TinyOwn& o, u32x4 (&w)[8], uint32_t (&geo)[8], uint32_t& st) {
-        // the owner's stored object checksum (records mode), beside its window
-        st = d.vstat && o.ix != kNoIdx ? load_u32_any(o.S - 4) : 0u;
-        static_for8([&](auto qc) {
-            constexpr int q = decltype(qc)::value;
-            geo[q] = swz_from<q>(o.geo);
-            const uint64_t A = (uint64_t(swz_from<q>(uint32_t(o.A >> 32))) << 32) |
-                               swz_from<q>(uint32_t(o.A));
-            const uint32_t e = ((geo[q] >> 8) & 0xF) + (geo[q] & 0xFF);   // E - A
-            const bool ok = geo[q] != 0 && uint32_t(gl) * 16 < e;
-            w[q] = load16(ok ? A + uint32_t(gl) * 16 : (geo[q] ? A : dummy));   // past E: zero rows
-        });
-    };
-
-    uint64_t r = wave;
-    TinyOwn o0 = load_own(r), o1 = load_own(r + nwaves);
-    // (issuing the first round's windows before the table fill was 1-2 %
-    // slower: the fill's loads queue behind them)
-    fill_plain(lds, 0, &g_tab.pos[0][0], 132 * 256);
-    if (__syncthreads_or(bad))
-        return false;
-    u32x4 wc[8];
-    uint32_t gc[8], sc;
-    issue(o0, wc, gc, sc);
-    const uint32_t* tab = reinterpret_cast<const uint32_t*>(lds);
-    for (; r < rounds; r += nwaves) {
-        const TinyOwn o2 = load_own(r + 2 * nwaves);
-        u32x4 wn[8];
-        uint32_t gn[8], sn = 0;
-        if (r + nwaves < rounds)
-            issue(o1, wn, gn, sn);
-        uint32_t mine = 0;
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const uint32_t len = gc[q] & 0xFF;
-            const int sa = int((gc[q] >> 8) & 0xF);
-            const int ds = sa - 16 * gl;                 // S - a
-            const int e = sa + int(len) - 16 * gl;       // E - a (<= 128)
-            const uint32_t ws[4] = {wc[q].x, wc[q].y, wc[q].z, wc[q].w};
-            uint32_t v[16];
-#if RAMCRC_TINY_TRIM
-            // Only lane 0 of the group holds bytes before S (ds = S - a is
-            // 0..15 there and negative elsewhere): h8 = bits to drop from the
-            // bottom of the lane's 128 bits.  Dword j drops clamp(h8 - 32 j,
-            // 0, 32) bits: one 64-bit shift makes the mask, 0 at 32.  The row
-            // base max(e - 4 j, 0) * 256 is one saturating subtract from
-            // max(e, 0) * 256.
-            const int h8 = max(ds, 0) * 8;
-            const uint32_t eb = uint32_t(max(e, 0)) << 10;   // bytes
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t drop = uint32_t(min(max(h8 - 32 * j, 0), 32));
-                const uint32_t x = ws[j] & uint32_t(~uint64_t(0) << drop);
-                const uint32_t base = __builtin_elementwise_sub_sat(eb, uint32_t(4096 * j));
-#pragma unroll
-                for (int t = 0; t < 4; t++) {
-#if RAMCRC_TINY_PROBE
-                    // bank-conflict probe (WRONG results): bank = lane & 31
-                    const uint32_t ad = ((base | (((x >> (8 * t)) & 0xFF) << 2)) & ~0x7Cu) |
-                                        ((uint32_t(lane) & 31) << 2);
-#else
-                    const uint32_t ad = base | (((x >> (8 * t)) & 0xFF) << 2);
-#endif
-                    v[4 * j + t] = *reinterpret_cast<const uint32_t*>(
-                        lds + ad + (kTinyRow0 - t) * 1024);
-                }
-            }
-#else
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t x = ws[j] & ~keep_lo(ds - 4 * j);
-                const uint32_t base = uint32_t(max(e - 4 * j, 0)) << 8;
-#pragma unroll
-                for (int t = 0; t < 4; t++)
-                    v[4 * j + t] = tab[base + ((x >> (8 * t)) & 0xFF) + (kTinyRow0 - t) * 256];
-            }
-#endif
-            const uint32_t t0 = xor3(v[0], v[1], v[2]), t1 = xor3(v[3], v[4], v[5]);
-            const uint32_t t2 = xor3(v[6], v[7], v[8]), t3 = xor3(v[9], v[10], v[11]);
-            const uint32_t t4 = xor3(v[12], v[13], v[14]);
-            uint32_t R = xor3(xor3(t0, t1, t2), xor3(t3, t4, v[15]), 0u);
-            R = group8_xor_all(R);
-            mine = gl == q ? R : mine;
-        }
-        // own slot: the initial state (byte k at distance len - k), or bytewise
-        if (o0.ix != kNoIdx) {
-            uint32_t R;
-            if (o0.len >= 4) {
-                const uint32_t ib = (o0.len + kTinyRow0) << 8;
-                const uint32_t in = o0.init;
-                R = mine ^ xor3(tab[ib + (in & 0xFF)], tab[ib - 256 + ((in >> 8) & 0xFF)],
-                                tab[ib - 512 + ((in >> 16) & 0xFF)]) ^
-                    tab[ib - 768 + (in >> 24)];
-            } else {
-                R = o0.init;
-                for (uint32_t k = 0; k < o0.len; k++)
-                    R = tab[(1 + kTinyRow0) * 256 + ((R ^ *(const gu8*)(o0.S + k)) & 0xFF)] ^ (R >> 8);
-            }
-            const uint32_t Rf = finalize ? ~R : R;
-            d.out[o0.ix] = Rf;
-            if (d.vstat && Rf != sc)
-                atomicAdd(&d.vstat[d.rec[o0.ix].x].bad_objects, 1u);
-        }
-        o0 = o1;
-        o1 = o2;
-        sc = sn;
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            wc[q] = wn[q];
-            gc[q] = gn[q];
-        }
-    }
-    return true;
-}
-
 // Probe builds only (RAMCRC_STAMPS=1, tools/stamps.py): lane 0 of every wave
 // records the 100 MHz real-time clock at k_entries' phase boundaries.
 #ifndef RAMCRC_STAMPS
@@ -2157,19 +2000,15 @@ __device__ unsigned long long g_stamps[kStampWaves * kStampSlots];
     } while (0)
 #endif
 
-// The tiny phases with conflict-free table lookups (RAMCRC_TINY_CF).  The
-// position table is laid out column-major, byte address 512 (255 - b) +
-// 4 (128 - m) for X^m(b) (g_tab.post), so a lookup's LDS bank is (128 - m)
-// mod 32 whatever the data byte.  Lane u of a group holds the window dwords
-// u, u + 8, u + 16, u + 24 (window offsets 32 j + 4 u), so the 8 lanes of a
-// group read 8 rows 4 apart: 8 banks of one residue class mod 4.  Each group
-// takes the bytes of its dwords in a rotated order, byte (k + c) & 3 at
-// instruction k with c = (e + g) & 3 (e the window-relative entry end, g the
-// group's index in its 32-lane half), which puts the 4 groups of a half on the
-// 4 residue classes: the 32 lanes of a ds_read_b32 group hit 32 banks.  Bytes
-// outside the entry are masked to 0 and complemented to column 255, whose
-// rows, and the 128 words after the table, are zero; so no zero rows and
-// no clamps are needed.
+// The tiny phases with conflict-free table lookups (RAMCRC_TINY_CF): the
+// window-relative table below puts a lookup's LDS bank on its window position,
+// whatever the data byte.  Lane u of a group holds the window dwords u, u + 8,
+// u + 16, u + 24 (window offsets 32 j + 4 u), so the 8 lanes of a group read
+// rows 4 apart; each group takes the bytes of its dwords in a rotated order
+// (byte (k + g) & 3 at instruction k, g the group's index in its 32-lane
+// half), which puts the 4 groups of a half on the 4 residue classes: the 32
+// lanes of a ds_read_b32 half hit 32 banks.  Bytes outside the entry are
+// masked to 0, and X^m(0) = 0.
 //
 // tiny_run_cf: bins 0-1, entries of one 128-byte window (all 100-byte log
 // entries).  tiny_multi: bins 2 .. kTinyK, entries of 2 .. kTinyK windows
@@ -2217,7 +2056,7 @@ __device__ __forceinline__ uint32_t tk_windows(uint32_t geo)
     return ((geo & 0x3FFu) - tk_tail(geo) + 127u) >> 7;
 }
 
-// RAMCRC_TINY_WR: the tiny phases' LDS holds X^(128 - q)(b) for window
+// The tiny phases' LDS holds X^(128 - q)(b) for window
 // position q at ((q >> 6) << 16) | (b << 8) | ((q & 63) << 2) -- the data byte
 // is address byte 1, so one v_perm forms an address from a per-lane constant
 // -- and X^-128 (4 x 256 words) after it.  A window's bytes are summed at their
@@ -2544,17 +2383,11 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
             w[q] = v;
         });
     };
-#if !RAMCRC_TINY_WR
-    // X^m(b) in the column-major table
-    auto tabv = [&](uint32_t m, uint32_t b) -> uint32_t {
-        return *reinterpret_cast<const uint32_t*>(lds + 512 * (255 - b) + 4 * (128 - m));
-    };
-#endif
 
     // RAMCRC_TINY_OVL: the table's basis words are loaded first, round 0's
     // windows issued as soon as its owners are known, and the table built
     // while those loads are in flight (the build waits for the basis alone)
-    constexpr bool kOvl = RAMCRC_TINY_OVL && RAMCRC_TINY_GEN && RAMCRC_TINY_WR;
+    constexpr bool kOvl = RAMCRC_TINY_OVL && RAMCRC_TINY_GEN;
 #if RAMCRC_TINY_GEN
     TinyBasis tb;
     if constexpr (kOvl)
@@ -2564,7 +2397,6 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
     TinyOwn o0 = load_own(r), o1 = load_own(r + nwaves);
     u32x4 wc[8];
     uint32_t gc[8], sc;
-#if RAMCRC_TINY_WR
 #if RAMCRC_TINY_GEN
     if constexpr (kOvl) {
         issue(o0, wc, gc, sc);
@@ -2586,9 +2418,6 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
     TwSel ts;
     if constexpr (kLsel)
         ts = TwSel(g4);
-#else
-    fill_plain(lds, 0, g_tab.post, 256 * 128 + 128);
-#endif
     if (__syncthreads_or(bad))
         return false;
     RAMCRC_STAMP(5);
@@ -2604,7 +2433,6 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
                 issue(o1, wn, gn, sn);
         }
         uint32_t mine = 0;
-#if RAMCRC_TINY_WR
         static_for8([&](auto qc) {
             constexpr int q = decltype(qc)::value;
             const uint32_t g = kRegeo ? swz_from<q>(o0.geo) : gc[q];
@@ -2616,53 +2444,10 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
                                   : tiny_win_wr<kLsel, false>(lds, wc[q], sa, e, rw, gl, g4, ts);
             mine = gl == uint32_t(q) ? R : mine;
         });
-#else
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const uint32_t sa = (gc[q] >> 8) & 0xF;
-            const uint32_t e = sa + (gc[q] & 0xFF);           // window-relative end, <= 128
-            const uint32_t c = (e + g4) & 3;                  // byte rotation of this group
-            const uint32_t bb = 512 - 4 * e + 16 * gl;        // 4 (128 - e + 4 u): row of offset 4 u
-            const uint32_t rot = __builtin_amdgcn_alignbyte(0x0C080400u, 0x0C080400u, c);
-            // byte k of the rotated dword sits at window offset 4 u + ((k + c) & 3)
-            // (row bits below 512 for every byte of the entry; a masked byte's
-            // column 255 is zero at every row, so OR-ing its larger row is safe)
-            uint32_t pk[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                pk[k] = bb + ((rot >> (8 * k)) & 0xFF);
-            // tail: dword j keeps its bytes before E, clamp(e - 32 j - 4 u, 0, 4)
-            const int z = 32 - 8 * int(e) + 32 * int(gl);   // bits to drop from dword 0's top
-            // head: window bytes before S lie in dword 0 of lanes 0-3
-            const uint32_t hd = uint32_t(min(max(8 * (int(sa) - 4 * int(gl)), 0), 32));
-            const uint32_t ws[4] = {wc[q].x, wc[q].y, wc[q].z, wc[q].w};
-            uint32_t v[16];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t sh = uint32_t(min(max(z + 256 * j, 0), 32));
-                uint32_t keep = uint32_t(uint64_t(0xFFFFFFFFu) >> sh);
-                if (j == 0)
-                    keep &= uint32_t(~uint64_t(0) << hd);
-                const uint32_t xb = ~(ws[j] & keep);          // masked bytes -> column 255
-                const uint32_t xr = __builtin_amdgcn_alignbyte(xb, xb, c);
-#pragma unroll
-                for (int k = 0; k < 4; k++)
-                    v[4 * j + k] = *reinterpret_cast<const uint32_t*>(
-                        lds + ((((xr >> (8 * k)) & 0xFF) << 9) | pk[k]) + 128 * j);
-            }
-            const uint32_t t0 = xor3(v[0], v[1], v[2]), t1 = xor3(v[3], v[4], v[5]);
-            const uint32_t t2 = xor3(v[6], v[7], v[8]), t3 = xor3(v[9], v[10], v[11]);
-            const uint32_t t4 = xor3(v[12], v[13], v[14]);
-            uint32_t R = xor3(xor3(t0, t1, t2), xor3(t3, t4, v[15]), 0u);
-            R = group8_xor_all(R);
-            mine = gl == uint32_t(q) ? R : mine;
-        }
-#endif
         // own slot: the initial state (byte k at distance len - k), or bytewise
         if (o0.ix != kNoIdx) {
             uint32_t R;
             const uint32_t n = (o0.geo >> 16) & 0xFF;   // the entry's length
-#if RAMCRC_TINY_WR
             if (n >= 4) {
                 // the window sum moved from the window's end to the entry's end,
                 // e = S - A + n >= 4 bytes into the window
@@ -2674,18 +2459,6 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
                     R = *reinterpret_cast<const uint32_t*>(
                             lds + tw_addr(127, (R ^ *(const gu8*)(o0.S + k)) & 0xFF)) ^ (R >> 8);
             }
-#else
-            if (n >= 4) {
-                const uint32_t in = o0.init;
-                R = mine ^ xor3(tabv(n, in & 0xFF), tabv(n - 1, (in >> 8) & 0xFF),
-                                tabv(n - 2, (in >> 16) & 0xFF)) ^
-                    tabv(n - 3, in >> 24);
-            } else {
-                R = o0.init;
-                for (uint32_t k = 0; k < n; k++)
-                    R = tabv(1, (R ^ *(const gu8*)(o0.S + k)) & 0xFF) ^ (R >> 8);
-            }
-#endif
             const uint32_t Rf = finalize ? ~R : R;
             d.out[o0.ix] = Rf;
             if (d.vstat && Rf != sc)
