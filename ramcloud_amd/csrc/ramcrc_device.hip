@@ -970,9 +970,6 @@ constexpr int kPU = RAMCRC_PU;             // ping-pong depth (pipelined bins)
 #ifndef RAMCRC_TINY_OVL
 #define RAMCRC_TINY_OVL 1   // tiny phase: round 0's windows in flight while the table is built
 #endif
-#ifndef RAMCRC_TINY_PROBE
-#define RAMCRC_TINY_PROBE 0  // A/B only: conflict-free lookup addresses, wrong CRCs
-#endif
 constexpr uint32_t kNoIdx = 0xFFFFFFFFu;   // empty slot
 #ifndef RAMCRC_SPLIT
 #define RAMCRC_SPLIT 1   // k_entries: tiny and long phases on separate workgroups when a batch has both
