@@ -747,22 +747,6 @@ __device__ __forceinline__ bool replay_other(const u32x4& r)
     return hdr != 0 && !(type == RAMCRC_LOG_ENTRY_TYPE_OBJ && readable && !is_large(uint64_t(r.z) - 4));
 }
 
-// A walk record {segment, offset, length, header} the direct tiny path cannot
-// take by itself: a record k_obj_compare has work for, or an object whose
-// bytes [4, length) span more than one 128-byte window (the walk keeps
-// segments 16-byte aligned, so the window follows from the offset alone).
-// The fused replay call ORs this over every record its walk writes; when no
-// record is hard, the verify needs no binning (ramcrc_replay_verify_device).
-__device__ __forceinline__ bool replay_hard(uint32_t pos, uint32_t len, uint32_t hdr)
-{
-    const u32x4 r = {0u, pos, len, hdr};
-    if (replay_other(r))
-        return true;
-    if ((hdr & (0x3f | kRecOverlong)) != RAMCRC_LOG_ENTRY_TYPE_OBJ || len < kObjHeaderBytes)
-        return false;   // nothing to scan
-    const uint32_t s16 = (pos + 1 + ((hdr >> 6) & 3) + 1 + 4) & 15;   // S mod 16
-    return len - 4 >= 4 && s16 + (len - 4) > 128;
-}
 
 
 // Locate (entry, chunk) for global chunk index g in general mode.
@@ -951,6 +935,29 @@ constexpr int kSmallK = RAMCRC_SMALLK;     // bins 2..kSmallK: octets loaded one
 // ~500 B): the multi-window tiny phase (tiny_run_cf<true>); 1 = off (the short bins)
 constexpr int kTinyK = RAMCRC_TINY_K;
 static_assert(kTinyK >= 1 && kTinyK <= 7, "tiny windows: E - A (<= 128 kTinyK) fits 10 bits");
+
+// What a walk record {segment, offset, length, header} rules out for the
+// verify: bit 0, the direct one-window tiny path (a record k_obj_compare has
+// work for, or an object whose bytes [4, length) span more than one 128-byte
+// window -- the walk keeps segments 16-byte aligned, so the windows follow
+// from the offset alone); bit 1, the direct multi-window path (anything but
+// an object of 2 .. kTinyK windows).  The fused replay call ORs this over
+// every record its walk writes; unless both bits end up set the verify needs
+// no binning scatter (ramcrc_replay_verify_device, k_bin_count).
+constexpr uint32_t kHardAll = 3u;
+__device__ __forceinline__ uint32_t replay_hard(uint32_t pos, uint32_t len, uint32_t hdr)
+{
+    const u32x4 r = {0u, pos, len, hdr};
+    if (replay_other(r))
+        return kHardAll;
+    if ((hdr & (0x3f | kRecOverlong)) != RAMCRC_LOG_ENTRY_TYPE_OBJ || len < kObjHeaderBytes)
+        return 0u;   // nothing to scan
+    const uint32_t s16 = (pos + 1 + ((hdr >> 6) & 3) + 1 + 4) & 15;   // S mod 16
+    const uint32_t steps = (s16 + (len - 4) + 127) / 128;             // entry_steps
+    if (len - 4 < 4 || steps <= 1)
+        return 2u;   // one window (or bytewise): the tiny path
+    return steps <= uint32_t(kTinyK) ? 1u : kHardAll;
+}
 #ifndef RAMCRC_ENT_NT
 #define RAMCRC_ENT_NT 1
 #endif
@@ -1031,6 +1038,9 @@ constexpr uint64_t kBinWgsPerCu = RAMCRC_BIN_WGS_PER_CU;   // binning grid cap p
 // tiny windows: per-lane v_perm selectors instead of a v_alignbyte per dword
 // -- 0 never, 1 always, 2 where the round loop has no register prefetch
 #define RAMCRC_TINY_LSEL 2
+#endif
+#ifndef RAMCRC_TINY_DM
+#define RAMCRC_TINY_DM 1   // records batches whose objects all span 2 .. kTinyK windows: no scatter
 #endif
 #ifndef RAMCRC_TINY_M2
 #define RAMCRC_TINY_M2 1   // tiny_multi: bin 2 with two-window buffers and a ring of four
@@ -1135,6 +1145,9 @@ struct BinTable {
     uint64_t kcost[kNB];      // steps charged per octet of the bin (its largest step count)
     uint64_t direct_n;        // nonzero: every entry of this kTable batch is tiny; the tiny
                               // phase reads the caller's table in place (nothing scattered)
+    uint64_t direct_multi;    // nonzero: every active record of this records batch is an
+                              // object of 2 .. kTinyK windows (bin 2 holds them all); the
+                              // multi-window tiny phase reads the record table in place
     BinCounters ctr[2];       // per parity; copy p ^ 1 is zeroed by sequence p's k_bin_count
     uint64_t rescues;         // k_bin_one launches that aborted and were binned by the guarded scatter
 };
@@ -1228,10 +1241,13 @@ __device__ __forceinline__ uint32_t wave_bin_add(uint32_t* h, int b, bool active
 // wrapped: the k_entries hang of round 2.  Each log-scale bin's work estimate
 // now uses the bin's upper bound (bin_kmax).
 // sum (nullable; records mode, ramcrc_replay_verify_device): the walk's
-// replay_hard summary.  0: every record is inactive or a one-window object, so
-// the histogram is "all tiny" without reading the table -- the scatter then
-// publishes the direct path, which re-checks every record (a record that is
-// not tiny refuses the launch), and the plan and compare kernels find nothing.
+// replay_hard bits.  Bit 0 clear: every record is inactive or a one-window
+// object, so the histogram is "all tiny" without reading the table -- the
+// scatter then publishes the direct path, which re-checks every record (a
+// record that is not tiny refuses the launch), and the plan and compare
+// kernels find nothing.  Bit 1 clear: every record is inactive or an object
+// of 2 .. kTinyK windows -- "all in bin 2", the direct multi-window path,
+// which re-checks the same way.
 template <int kMode>
 __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, int skip_large,
                                                         const uint32_t* sum)
@@ -1258,9 +1274,14 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
             nx.flag = 0;
         }
     }
-    if (sum && *sum == 0) {
+    // the fused replay's summary (replay_hard bits over every walk record):
+    // no record beyond one window -- all in bin 1, the direct tiny path; none
+    // but objects of 2 .. kTinyK windows -- all in bin 2, the direct
+    // multi-window path (bin_layout tells them apart by the bin)
+    const uint32_t sv = sum ? *sum : 3u;
+    if (!(sv & 1u) || (RAMCRC_TINY_DM && kTinyK >= 2 && !(sv & 2u))) {
         if (blockIdx.x == 0 && threadIdx.x == 0)
-            ctr.hist[1] = uint32_t(entry_count<kMode>(d));
+            ctr.hist[(sv & 1u) ? 2 : 1] = uint32_t(entry_count<kMode>(d));
         return;
     }
     for (int t = threadIdx.x; t < kNB; t += blockDim.x)
@@ -1379,7 +1400,7 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
 struct BinScratch {
     uint64_t start[kNB], count[kNB];
     uint64_t wpos[4], witem[4];
-    uint32_t direct;
+    uint32_t direct, multi;
 };
 
 // Returns false (uniformly) when the histogram asks for more sorted slots
@@ -1398,23 +1419,31 @@ __device__ __forceinline__ uint32_t ld_agent(const uint32_t* p)
 }
 
 __device__ __forceinline__ bool bin_layout(const Sorted& so, BinScratch& sc, bool publish,
-                                          uint64_t direct_n, const uint32_t* hist = nullptr)
+                                          uint64_t direct_n, const uint32_t* hist = nullptr,
+                                          uint64_t multi_n = 0)
 {
     BinTable* bt = so.bt;
     const BinCounters& ctr = bt->ctr[so.par];
     const int b = threadIdx.x, lane = b & 63, w = b >> 6;
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0) {
+        const uint64_t inact = ld_agent(&ctr.ninact);
         sc.direct = direct_n && uint64_t(hist ? hist[0] : ld_agent(&ctr.hist[0])) +
-                                        (hist ? hist[1] : ld_agent(&ctr.hist[1])) +
-                                        ld_agent(&ctr.ninact) == direct_n;
+                                        (hist ? hist[1] : ld_agent(&ctr.hist[1])) + inact == direct_n;
+        // multi_n (records batches): every active record in bin 2 -- the
+        // direct multi-window path reads the record table in place
+        sc.multi = !sc.direct && multi_n &&
+                   uint64_t(hist ? hist[2] : ld_agent(&ctr.hist[2])) + inact == multi_n;
+    }
     __syncthreads();
-    const bool direct = sc.direct;
-    if (publish && threadIdx.x == 0)
+    const bool direct = sc.direct, multi = sc.multi;
+    if (publish && threadIdx.x == 0) {
         bt->direct_n = direct ? direct_n : 0;
+        bt->direct_multi = multi ? multi_n : 0;
+    }
     uint64_t cnt = 0, kc = 0, ps = 0, is = 0, pos_c = 0, item_c = 0;
     if (b < 256) {
         if (b < kNB) {
-            cnt = direct ? 0 : (hist ? hist[b] : ld_agent(&ctr.hist[b]));
+            cnt = direct || multi ? 0 : (hist ? hist[b] : ld_agent(&ctr.hist[b]));
             kc = b <= 32 ? uint64_t(b == 0 ? 1 : b) : bin_kmax(b);
         }
         const uint64_t oct = (cnt + kG - 1) / kG;
@@ -1514,10 +1543,11 @@ __global__ __launch_bounds__(kThreads) void k_bin_scatter(BatchDesc d, Sorted so
     __syncthreads();
     if (!bin_layout(so, sc, blockIdx.x == 0,
                     (kMode == kTable || kMode == kRecords) && RAMCRC_TINY_CF ? entry_count<kMode>(d) : 0,
-                    rescue ? tot : nullptr))
+                    rescue ? tot : nullptr,
+                    kMode == kRecords && RAMCRC_TINY_DM && kTinyK >= 2 ? entry_count<kMode>(d) : 0))
         return;   // corrupted histogram: nothing is scattered, k_entries refuses
-    if (sc.direct)
-        return;   // all tiny: k_entries reads the table in place
+    if (sc.direct || sc.multi)
+        return;   // all tiny / all of 2 .. kTinyK windows: k_entries reads the table in place
     unsigned long long* cursor = reinterpret_cast<unsigned long long*>(ctr.cursor);
     const uint64_t tile = uint64_t(blockDim.x) * kBinPer;
     const uint64_t n = entry_count<kMode>(d);
@@ -2488,7 +2518,11 @@ __device__ __forceinline__ bool tiny_run_cf(const BatchDesc& d, const Sorted& so
 // with kK = 2 and a ring of 4 -- three entries in flight per group for the
 // registers the general loop spends on two buffers of four windows; bins 3 ..
 // kTinyK with kK = kTinyK and two buffers.
-template <int kK, int kDepth>
+// kDirect: a records batch read in place (BinTable::direct_multi), record i
+// at slot i; a record that is not an object of 2 .. kTinyK windows refuses the
+// launch (the summary that chose this path was wrong), as the direct tiny
+// path does.
+template <int kK, int kDepth, bool kDirect = false>
 __device__ __forceinline__ void tiny_multi_run(const BatchDesc& d, const Sorted& so, const uint8_t* lds,
                                                uint32_t blk, uint32_t nblk, uint64_t s0, uint64_t s1)
 {
@@ -2512,11 +2546,26 @@ __device__ __forceinline__ void tiny_multi_run(const BatchDesc& d, const Sorted&
         TinyRaw w;
         const uint64_t sl = s0 + r * 64 + uint32_t(lane);
         const bool in = r < rounds && sl < s1;
-        const uint64_t sc = in ? sl : s0;
-        w.dd = so.desc[sc];
-        const uint32_t ix = so.idx[sc];
-        w.ix = in ? ix : kNoIdx;
-        w.init = d.init ? so.init[sc] : 0xFFFFFFFFu;
+        if constexpr (kDirect) {
+            uint64_t S = 0, E = 0;
+            bool act = in && record_range(d, d.rec[sl], S, E);
+            if (act) {
+                const uint64_t k = entry_steps(S, E);
+                if (k < 2 || k > uint64_t(kTinyK)) {
+                    atomicOr(so.status, kStatusSticky | kStatusBins);   // refuse, write nothing
+                    act = false;
+                }
+            }
+            w.dd = u32x4{uint32_t(S), uint32_t(S >> 32), uint32_t(E), uint32_t(E >> 32)};
+            w.ix = act ? uint32_t(sl) : kNoIdx;
+            w.init = d.init && in ? d.init[sl] : 0xFFFFFFFFu;
+        } else {
+            const uint64_t sc = in ? sl : s0;
+            w.dd = so.desc[sc];
+            const uint32_t ix = so.idx[sc];
+            w.ix = in ? ix : kNoIdx;
+            w.init = d.init ? so.init[sc] : 0xFFFFFFFFu;
+        }
         return w;
     };
     auto own_of = [&](const TinyRaw& w) -> TinyCf {
@@ -2660,6 +2709,10 @@ __device__ __forceinline__ void tiny_multi(const BatchDesc& d, const Sorted& so,
                                            uint32_t blk, uint32_t nblk)
 {
     if constexpr (kTinyK >= 2) {
+        if (RAMCRC_TINY_DM && so.bt->direct_multi) {
+            tiny_multi_run<kTinyK, 2, true>(d, so, lds, blk, nblk, 0, so.bt->direct_multi);
+            return;
+        }
         const uint64_t s0 = so.bt->start[2], s1 = so.bt->start[kTinyK + 1];
         if (s0 == s1)
             return;   // uniform
@@ -3148,7 +3201,8 @@ __global__ __launch_bounds__(kEntWaves * kWaveSize, 1) void k_entries(BatchDesc 
             atomicOr(so.status, kStatusSticky | kStatusBins);
     };
     RAMCRC_STAMP(0);
-    const bool have_tk = kTinyK >= 2 && !so.bt->direct_n && so.bt->start[kTinyK + 1] != so.bt->start[2];
+    const bool have_tk = kTinyK >= 2 && !so.bt->direct_n &&
+                         (so.bt->direct_multi || so.bt->start[kTinyK + 1] != so.bt->start[2]);
     // Role split (round 5, RAMCRC_SPLIT): when a batch has both tiny and long
     // entries, workgroups < T run only the tiny phases (filling only their
     // table) and the others only the long phase, so the two overlap and no
@@ -3698,7 +3752,7 @@ struct WalkDesc {
     unsigned long long* n_entries;
     const uint32_t* only;   // nullable: walk only the segments with only[seg] != 0
     uint64_t* seg_base;     // nullable: per segment, the first slot of its records
-    uint32_t* sum;          // nullable: ORed with 1 when a written record is replay_hard
+    uint32_t* sum;          // nullable: ORed with the written records' replay_hard bits
 };
 
 // CRC32C update by the m (1..4) bytes in the low end of v; t[j][b] = X^(j+1)(b).
@@ -3748,7 +3802,7 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
         xm[t] = g_tab.xmeta[t];
     __syncthreads();
     const int lane = threadIdx.x;
-    bool hard = false;   // a record this wave wrote is replay_hard (w.sum)
+    uint32_t hard = 0;   // replay_hard bits of the records this wave wrote (w.sum)
 
     for (uint64_t seg = blockIdx.x; seg < w.nseg; seg += gridDim.x) {
         if (w.only && !w.only[seg])
@@ -3806,7 +3860,7 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
                 const unsigned long long b = rbase + rdone;
                 if (lane < int(nrec) && b + lane < w.cap) {
                     w.entries[b + lane] = u32x4{uint32_t(seg), rpos, rlen, rinfo};
-                    hard = hard || (w.sum && replay_hard(rpos, rlen, rinfo));
+                    hard |= w.sum ? replay_hard(rpos, rlen, rinfo) : 0u;
                 }
                 rdone += nrec;
             }
@@ -3941,8 +3995,11 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
         }
         }   // pass
     }
-    if (w.sum && __ballot(hard) && lane == 0)
-        atomicOr(w.sum, 1u);
+    {
+        const uint32_t hw = (__ballot(hard & 1u) ? 1u : 0u) | (__ballot(hard & 2u) ? 2u : 0u);
+        if (w.sum && hw && lane == 0)
+            atomicOr(w.sum, hw);
+    }
 }
 
 // ------------------------------------------------- parallel segment walk
@@ -4116,13 +4173,14 @@ __device__ __forceinline__ PWalk walk_geo(PWalk w)
 constexpr uint32_t kPartShiftMax = 20;
 constexpr int kProbeHops = 8;
 
-// The replay summary word (PWalk::sum) goes 0 -> 1 once per batch.  A wave
-// that saw a hard record reads it (coherently) and ORs only while it is 0:
-// with 1 KiB objects every wave has one, and 32K same-address atomics cost
-// 175 us per batch when k_walk_copy made them (profiles/r05/replayfix).
+// The replay summary word (PWalk::sum, replay_hard bits) only gains bits
+// within a batch.  A wave reads it (coherently) and ORs only the bits it
+// would add: with 1 KiB objects every wave has hard records, and 32K
+// same-address atomics cost 175 us per batch when k_walk_copy made them
+// (profiles/r05/replayfix).  No word: everything counts as seen.
 __device__ __forceinline__ uint32_t walk_sum_seen(const uint32_t* sum)
 {
-    return sum ? __hip_atomic_load(sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 1u;
+    return sum ? __hip_atomic_load(sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kHardAll;
 }
 
 __global__ __launch_bounds__(kWaveSize) void k_walk_probe(PWalk w, uint32_t forced, uint32_t* geo)
@@ -4542,13 +4600,13 @@ struct TableSink {
     u32x4* out;
     uint64_t n;
     uint32_t seg;
-    bool* hard;   // nullable: set when a written record is replay_hard
+    uint32_t* hard;   // nullable: ORed with the written records' replay_hard bits
     __device__ void operator()(uint32_t idx, uint32_t pos, uint32_t len, uint32_t hdr) const
     {
         if (idx < n) {
             out[idx] = u32x4{seg, pos, len, hdr};
-            if (hard && replay_hard(pos, len, hdr))
-                *hard = true;
+            if (hard)
+                *hard |= replay_hard(pos, len, hdr);
         }
     }
 };
@@ -5192,7 +5250,7 @@ __global__ __launch_bounds__(256) void k_walk_emit(PWalk w0)
     }
     const bool chase = emit && (r.flags & (kPartChase | kPartSpill));
     const uint32_t pre = emit && !chase ? r.pre : 0u;
-    bool hard = false;
+    uint32_t hard = 0;
     if (chase || pre) {
         const uint32_t k = uint32_t(i - seg * w.nparts);
         const uint32_t B = k << w.pshift;
@@ -5206,8 +5264,11 @@ __global__ __launch_bounds__(256) void k_walk_emit(PWalk w0)
                             w.sum ? &hard : nullptr},
                   chase ? (1u << w.pshift) : pre);
     }
-    if (w.sum && __ballot(hard) && (threadIdx.x & (kWaveSize - 1)) == 0 && !walk_sum_seen(w.sum))
-        atomicOr(w.sum, 1u);
+    if (w.sum) {
+        const uint32_t hw = (__ballot(hard & 1u) ? 1u : 0u) | (__ballot(hard & 2u) ? 2u : 0u);
+        if (hw && (threadIdx.x & (kWaveSize - 1)) == 0 && (hw & ~walk_sum_seen(w.sum)))
+            atomicOr(w.sum, hw);
+    }
 }
 
 // C': the scratch records of the parts accepted without a second walk.  One
@@ -5235,7 +5296,7 @@ __global__ __launch_bounds__(256) void k_walk_copy(PWalk w0)
     // fix-up instead -- the last hard index per part, counted from each
     // accepted part's cut -- measured 1 % slower: profiles/r05/replayfix.)
     const uint32_t seen = walk_sum_seen(w.sum);
-    bool hard = false;
+    uint32_t hard = 0;
     for (uint64_t b0 = (uint64_t(blockIdx.x) * (blockDim.x / kWaveSize) +
                         __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveSize)) * kCopyU;
          b0 < nblk; b0 += nwave * kCopyU) {
@@ -5289,12 +5350,15 @@ __global__ __launch_bounds__(256) void k_walk_copy(PWalk w0)
             const uint64_t dst = sbase[u] + r[u].rec + r[u].pre + (ri - r[u].cut);
             if (dst < w.cap) {
                 w.entries[dst] = u32x4{uint32_t(part[u] / w.nparts), v[u].x, v[u].y >> 8, v[u].y & 0xFF};
-                hard = hard || (!seen && replay_hard(v[u].x, v[u].y >> 8, v[u].y & 0xFF));
+                hard |= seen != kHardAll ? replay_hard(v[u].x, v[u].y >> 8, v[u].y & 0xFF) : 0u;
             }
         }
     }
-    if (!seen && __ballot(hard) && lane == 0)
-        atomicOr(w.sum, 1u);
+    {
+        const uint32_t hw = (__ballot(hard & 1u) ? 1u : 0u) | (__ballot(hard & 2u) ? 2u : 0u);
+        if ((hw & ~seen) && lane == 0)
+            atomicOr(w.sum, hw);
+    }
 }
 
 // ObjectManager::replaySegment's checksum checks on the walk records of the

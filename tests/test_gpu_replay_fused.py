@@ -101,3 +101,35 @@ def test_fused_equals_split_mixed_values(ramcrc):
         assert list(fs[:, 3]) == [0, 0, 0, 1, 0, 0, 0, 0]
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("vlen", [128, 256])
+def test_fused_multi_window_direct(ramcrc, vlen):
+    """128 B and 256 B values: every object spans two (three) windows, so the
+    fused call's summary sends the batch to the direct multi-window path --
+    the count pass puts every record in bin 2 without reading the table and
+    nothing is scattered -- with one damaged object and one damaged
+    certificate; identical to the split calls (which bin the records)."""
+    from ramcloud_amd import segments
+    nseg = 12
+    ctx = ramcrc.Context(0)
+    try:
+        d, certs, per, ck = _batch(ramcrc, ctx, nseg, vlen, first_seed=0x1281 + vlen)
+        eb = segments.entry_bytes(vlen)
+        d[4 * SEG + 333 * eb + eb - 5] ^= 0x08
+        certs[7, 1] ^= 0x200
+        cap = nseg * per + 1024
+        fs, fn, ft, fc = _run(ramcrc, ctx, d, certs, nseg, cap, fused=True)
+        _, _, hist, par_next = ctx.debug_bins()
+        assert int(hist[par_next ^ 1][2]) == fn   # the shortcut: all records in bin 2
+        ss, sn, st, sc = _run(ramcrc, ctx, d, certs, nseg, cap, fused=False)
+        assert fn == sn == nseg * per
+        assert np.array_equal(fs, ss)
+        assert np.array_equal(ft, st)
+        assert np.array_equal(fc, sc)
+        bad = np.zeros(nseg, np.uint32)
+        bad[4] = 1
+        assert np.array_equal(fs[:, 3], bad)
+        assert fs[7, 0] & segments.SEG_BAD_CHECKSUM and not fs[7, 0] & segments.SEG_OK
+    finally:
+        ctx.close()
