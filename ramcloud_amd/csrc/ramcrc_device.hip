@@ -941,7 +941,8 @@ static_assert(kTinyK >= 1 && kTinyK <= 7, "tiny windows: E - A (<= 128 kTinyK) f
 // work for, or an object whose bytes [4, length) span more than one 128-byte
 // window -- the walk keeps segments 16-byte aligned, so the windows follow
 // from the offset alone); bit 1, the direct multi-window path (anything but
-// an object of 2 .. kTinyK windows).  The fused replay call ORs this over
+// an object of 2 .. kTinyK windows); bit 2, an object of 3 or more windows.
+// The fused replay call ORs this over
 // every record its walk writes; unless both bits end up set the verify needs
 // no binning scatter (ramcrc_replay_verify_device, k_bin_count).
 constexpr uint32_t kHardAll = 3u;
@@ -956,7 +957,9 @@ __device__ __forceinline__ uint32_t replay_hard(uint32_t pos, uint32_t len, uint
     const uint32_t steps = (s16 + (len - 4) + 127) / 128;             // entry_steps
     if (len - 4 < 4 || steps <= 1)
         return 2u;   // one window (or bytewise): the tiny path
-    return steps <= uint32_t(kTinyK) ? 1u : kHardAll;
+    // (bit 2: more than two windows -- the direct multi-window path then
+    // takes the general loop instead of the two-window ring)
+    return steps <= 2 ? 1u : (steps <= uint32_t(kTinyK) ? 5u : kHardAll | 4u);
 }
 #ifndef RAMCRC_ENT_NT
 #define RAMCRC_ENT_NT 1
@@ -1131,7 +1134,7 @@ struct BinCounters {
     uint32_t nother;          // records mode: records k_obj_compare has work for (replay_other)
     uint32_t arrive;          // k_bin_one: workgroups past their histogram atomics
     uint32_t flag;            // k_bin_one: 0, then kBinGo (last arrival) or kBinAbort (a stall)
-    uint32_t pad_;
+    uint32_t wide;            // fused replay, direct multi-window path: some object of 3 .. kTinyK windows
     uint32_t hs[kBinSlices][kNB];   // k_bin_one: histogram per slice of workgroups
     uint32_t arr[kBinSlices];       // k_bin_one: arrivals per slice
 };
@@ -1148,6 +1151,7 @@ struct BinTable {
     uint64_t direct_multi;    // nonzero: every active record of this records batch is an
                               // object of 2 .. kTinyK windows (bin 2 holds them all); the
                               // multi-window tiny phase reads the record table in place
+    uint64_t direct_multi_k2; // ... and none spans more than two windows (the two-window ring)
     BinCounters ctr[2];       // per parity; copy p ^ 1 is zeroed by sequence p's k_bin_count
     uint64_t rescues;         // k_bin_one launches that aborted and were binned by the guarded scatter
 };
@@ -1270,6 +1274,7 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
             nx.nlarge = 0;
             nx.ninact = 0;
             nx.nother = 0;
+            nx.wide = 0;
             nx.arrive = 0;
             nx.flag = 0;
         }
@@ -1280,8 +1285,10 @@ __global__ __launch_bounds__(kThreads) void k_bin_count(BatchDesc d, Sorted so, 
     // multi-window path (bin_layout tells them apart by the bin)
     const uint32_t sv = sum ? *sum : 3u;
     if (!(sv & 1u) || (RAMCRC_TINY_DM && kTinyK >= 2 && !(sv & 2u))) {
-        if (blockIdx.x == 0 && threadIdx.x == 0)
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
             ctr.hist[(sv & 1u) ? 2 : 1] = uint32_t(entry_count<kMode>(d));
+            ctr.wide = (sv & 4u) ? 1u : 0u;
+        }
         return;
     }
     for (int t = threadIdx.x; t < kNB; t += blockDim.x)
@@ -1439,6 +1446,7 @@ __device__ __forceinline__ bool bin_layout(const Sorted& so, BinScratch& sc, boo
     if (publish && threadIdx.x == 0) {
         bt->direct_n = direct ? direct_n : 0;
         bt->direct_multi = multi ? multi_n : 0;
+        bt->direct_multi_k2 = multi && !ld_agent(&ctr.wide);   // bin 2 proper: two windows at most
     }
     uint64_t cnt = 0, kc = 0, ps = 0, is = 0, pos_c = 0, item_c = 0;
     if (b < 256) {
@@ -1718,6 +1726,7 @@ __global__ __launch_bounds__(kThreads) void k_bin_one(BatchDesc d, Sorted so, in
             nx.nlarge = 0;
             nx.ninact = 0;
             nx.nother = 0;
+            nx.wide = 0;
             nx.arrive = 0;
             nx.flag = 0;
         }
@@ -2710,7 +2719,10 @@ __device__ __forceinline__ void tiny_multi(const BatchDesc& d, const Sorted& so,
 {
     if constexpr (kTinyK >= 2) {
         if (RAMCRC_TINY_DM && so.bt->direct_multi) {
-            tiny_multi_run<kTinyK, 2, true>(d, so, lds, blk, nblk, 0, so.bt->direct_multi);
+            if (RAMCRC_TINY_M2 && kTinyK > 2 && so.bt->direct_multi_k2)
+                tiny_multi_run<2, 4, true>(d, so, lds, blk, nblk, 0, so.bt->direct_multi);
+            else
+                tiny_multi_run<kTinyK, 2, true>(d, so, lds, blk, nblk, 0, so.bt->direct_multi);
             return;
         }
         const uint64_t s0 = so.bt->start[2], s1 = so.bt->start[kTinyK + 1];
@@ -3996,7 +4008,8 @@ __global__ __launch_bounds__(kWaveSize) void k_seg_walk(WalkDesc w)
         }   // pass
     }
     {
-        const uint32_t hw = (__ballot(hard & 1u) ? 1u : 0u) | (__ballot(hard & 2u) ? 2u : 0u);
+        const uint32_t hw = (__ballot(hard & 1u) ? 1u : 0u) | (__ballot(hard & 2u) ? 2u : 0u) |
+                           (__ballot(hard & 4u) ? 4u : 0u);
         if (w.sum && hw && lane == 0)
             atomicOr(w.sum, hw);
     }
@@ -5265,7 +5278,8 @@ __global__ __launch_bounds__(256) void k_walk_emit(PWalk w0)
                   chase ? (1u << w.pshift) : pre);
     }
     if (w.sum) {
-        const uint32_t hw = (__ballot(hard & 1u) ? 1u : 0u) | (__ballot(hard & 2u) ? 2u : 0u);
+        const uint32_t hw = (__ballot(hard & 1u) ? 1u : 0u) | (__ballot(hard & 2u) ? 2u : 0u) |
+                           (__ballot(hard & 4u) ? 4u : 0u);
         if (hw && (threadIdx.x & (kWaveSize - 1)) == 0 && (hw & ~walk_sum_seen(w.sum)))
             atomicOr(w.sum, hw);
     }
@@ -5350,12 +5364,13 @@ __global__ __launch_bounds__(256) void k_walk_copy(PWalk w0)
             const uint64_t dst = sbase[u] + r[u].rec + r[u].pre + (ri - r[u].cut);
             if (dst < w.cap) {
                 w.entries[dst] = u32x4{uint32_t(part[u] / w.nparts), v[u].x, v[u].y >> 8, v[u].y & 0xFF};
-                hard |= seen != kHardAll ? replay_hard(v[u].x, v[u].y >> 8, v[u].y & 0xFF) : 0u;
+                hard |= (seen & kHardAll) != kHardAll ? replay_hard(v[u].x, v[u].y >> 8, v[u].y & 0xFF) : 0u;
             }
         }
     }
     {
-        const uint32_t hw = (__ballot(hard & 1u) ? 1u : 0u) | (__ballot(hard & 2u) ? 2u : 0u);
+        const uint32_t hw = (__ballot(hard & 1u) ? 1u : 0u) | (__ballot(hard & 2u) ? 2u : 0u) |
+                           (__ballot(hard & 4u) ? 4u : 0u);
         if ((hw & ~seen) && lane == 0)
             atomicOr(w.sum, hw);
     }
