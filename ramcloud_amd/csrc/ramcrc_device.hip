@@ -5293,6 +5293,9 @@ __global__ __launch_bounds__(256) void k_walk_emit(PWalk w0)
 // each level's loads for all of them together.
 static_assert(kPartRec == kWaveSize, "k_walk_copy: one lane per record of a block");
 
+#ifndef RAMCRC_COPY_NT
+#define RAMCRC_COPY_NT 1   // k_walk_copy: nontemporal record stores (replay 64 B +1.7 %)
+#endif
 #ifndef RAMCRC_COPY_U
 #define RAMCRC_COPY_U 4
 #endif
@@ -5363,7 +5366,15 @@ __global__ __launch_bounds__(256) void k_walk_copy(PWalk w0)
                 continue;
             const uint64_t dst = sbase[u] + r[u].rec + r[u].pre + (ri - r[u].cut);
             if (dst < w.cap) {
-                w.entries[dst] = u32x4{uint32_t(part[u] / w.nparts), v[u].x, v[u].y >> 8, v[u].y & 0xFF};
+                const u32x4 rec = {uint32_t(part[u] / w.nparts), v[u].x, v[u].y >> 8, v[u].y & 0xFF};
+#if RAMCRC_COPY_NT
+                // streamed: not read back by this kernel.  (The same for the
+                // part walk's scratch stores was 8 % slower: k_walk_copy reads
+                // that scratch back while it is still in the caches.)
+                __builtin_nontemporal_store(rec, &w.entries[dst]);
+#else
+                w.entries[dst] = rec;
+#endif
                 hard |= (seen & kHardAll) != kHardAll ? replay_hard(v[u].x, v[u].y >> 8, v[u].y & 0xFF) : 0u;
             }
         }
