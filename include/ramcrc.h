@@ -56,6 +56,11 @@ enum {
  * Without it the raw running state (Crc32C::result, :259) is returned, which
  * callers use to keep chaining (src/LogDigest.cc:75-80, src/Segment.cc:677-681). */
 #define RAMCRC_FINALIZE 1u
+/* Any other flag bit is RAMCRC_EINVAL.  Round 4's RAMCRC_ORDERED (2) and its
+ * ordered entry points were removed in round 5; a caller
+ * built against that header gets EINVAL instead of a silently ignored flag.
+ * RAMCRC_ABI_VERSION counts such removals. */
+#define RAMCRC_ABI_VERSION 6
 
 /* ---------------------------------------------------------------- host --- */
 

@@ -20,7 +20,10 @@ LIB = os.path.join(LIBDIR, "libramcrc.so")
 ARCH = "gfx950"
 
 SOURCES = ["ramcrc_device.hip", "ramcrc_host.cc", "ramcrc_shard.hip", "ramcrc_fill.hip"]
-HEADERS = ["gf2.h", "walk_rules.h", "shard_plan.h"]
+HEADERS = ["gf2.h", "walk_rules.h", "shard_plan.h",
+           # parts of ramcrc_device.hip (one translation unit)
+           "dev_common.inc", "dev_chunks.inc", "dev_bins.inc", "dev_entries.inc",
+           "dev_plan.inc", "dev_host.inc", "dev_walk.inc", "dev_checks.inc"]
 
 
 def hipcc():
@@ -31,6 +34,18 @@ def hipcc():
 
 
 SHA_MARKER = b"src_sha="
+
+# Knobs whose non-default values gave wrong results or skipped work in earlier
+# rounds' A/B probes.  The knobs are gone from the sources; a variant naming
+# one is refused here, and ramcrc.lib() refuses a library whose build_info
+# reports one (RAMCRC_LIB), so no bench line or test can run such a build.
+UNSAFE_DEFINES = ("RAMCRC_PROBE_", "RAMCRC_WALK_DEBUG", "RAMCRC_BIN_RESCUE", "RAMCRC_NO_CAPTURE")
+
+
+def unsafe_defines(defines):
+    """The entries of `defines` (or a build_info "defines=" list) that name an
+    unsafe knob."""
+    return [d for d in defines if d.startswith(UNSAFE_DEFINES)]
 
 
 def _deps():
@@ -86,7 +101,11 @@ def _compile(out, defines=(), verbose=False):
     flags = _flags(defines)
     cmd = [hipcc()] + [f for f in flags if f != "-ldl"]
     cmd += ["-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
+    if unsafe_defines(defines):
+        raise ValueError(f"refusing a build with unsafe knobs: {unsafe_defines(defines)}")
     cmd += [f'-DRAMCRC_SRC_SHA="{source_sha(defines)}"']
+    if defines:
+        cmd += [f'-DRAMCRC_DEFINES="{",".join(defines)}"']
     cmd += [os.path.join(CSRC, s) for s in SOURCES]
     cmd += ["-ldl", "-o", tmp]
     if verbose:

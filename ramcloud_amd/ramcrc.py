@@ -62,6 +62,8 @@ def lib():
     # caller on torch's runtime.
     import torch  # noqa: F401
     L = _c.CDLL(path)
+    if path != _build.LIB:
+        _check_variant(L, path)
     vp, u32, u64, i32 = _c.c_void_p, _c.c_uint32, _c.c_uint64, _c.c_int
     sig = {
         "ramcrc_update_hw": (u32, [u32, vp, u64]),
@@ -123,6 +125,27 @@ def lib():
         f.argtypes = args
     _lib = L
     return L
+
+
+def build_defines(info):
+    """The -D knobs a library was built with, from its ramcrc_build_info()."""
+    if " defines=" not in info:
+        return []
+    d = info.split(" defines=", 1)[1].split()
+    return d[0].split(",") if d and d[0] != "none" else []
+
+
+def _check_variant(L, path):
+    """RAMCRC_LIB: only A/B variants of this tree's table that compute exact
+    results (build.UNSAFE_DEFINES) may replace the product library."""
+    f = L.ramcrc_build_info
+    f.restype = _c.c_char_p
+    info = f().decode("ascii", "replace")
+    if "src_sha=" not in info:
+        raise RamcrcError(f"RAMCRC_LIB={path} is not a libramcrc build")
+    bad = _build.unsafe_defines(build_defines(info))
+    if bad:
+        raise RamcrcError(f"RAMCRC_LIB={path} is a probe build ({bad}); refusing to load it")
 
 
 def exported_symbols():

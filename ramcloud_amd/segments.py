@@ -162,12 +162,11 @@ class RecoveryVerify:
                 self.check(stream)
             return st
         self.walk(d_segments, d_certs, stream)
-        if self.grow:
-            self.ctx.check(stream)
-            n = int(self.n_entries.item())
-            if n > self.entries.shape[0]:
-                self._alloc(n + n // 8 + self.nseg)
-                self.walk(d_segments, d_certs, stream)
+        self.ctx.check(stream)
+        n = int(self.n_entries.item())
+        if n > self.entries.shape[0]:
+            self._alloc(n + n // 8 + self.nseg)
+            self.walk(d_segments, d_certs, stream)
         st = self.verify_objects(d_segments, stream)
         if check:
             self.check(stream)

@@ -4,19 +4,22 @@
 
 Kept out of build.py so that editing this bookkeeping never changes the
 product library's source hash (build.source_sha covers only the sources,
-headers and compile flags of the default build)."""
+headers and compile flags of the default build).
+
+Every entry changes a knob away from its default and gives exact results:
+tests/test_variants.py checks both (knob present in the sources, value not the
+default, no knob in build.UNSAFE_DEFINES).  Libraries built from this table
+report their defines in ramcrc_build_info(), and ramcrc.lib() refuses one that
+names an unsafe knob."""
 
 VARIANTS = {
-    "u4_c18": ["RAMCRC_UNROLL=4", "RAMCRC_CHUNK_SHIFT=18"],
-    "u2_c18": ["RAMCRC_UNROLL=2", "RAMCRC_CHUNK_SHIFT=18"],
-    "u6_c18": ["RAMCRC_UNROLL=6", "RAMCRC_CHUNK_SHIFT=18"],
-    "u4_c19": ["RAMCRC_UNROLL=4", "RAMCRC_CHUNK_SHIFT=19"],
-    "u4_c17": ["RAMCRC_UNROLL=4", "RAMCRC_CHUNK_SHIFT=17"],
-    "u4_c20": ["RAMCRC_UNROLL=4", "RAMCRC_CHUNK_SHIFT=20"],
+    "u2": ["RAMCRC_UNROLL=2"],
+    "u6": ["RAMCRC_UNROLL=6"],
+    "c19": ["RAMCRC_CHUNK_SHIFT=19"],
+    "c17": ["RAMCRC_CHUNK_SHIFT=17"],
+    "c20": ["RAMCRC_CHUNK_SHIFT=20"],
     # parallel-walk sync search (k_walk_sync)
-    "walkdbg": ["RAMCRC_WALK_DEBUG=1"],
     "fw32": ["RAMCRC_FIX_WIN_KIB=32"],
-    "nocap": ["RAMCRC_NO_CAPTURE=1"],
     "ew12": ["RAMCRC_ENT_WAVES=12"],
     "sh4": ["RAMCRC_SYNC_HOPS=4"],
     "sh5": ["RAMCRC_SYNC_HOPS=5"],
@@ -33,7 +36,6 @@ VARIANTS = {
     "ss8": ["RAMCRC_SYNC_STAGE_KIB=8"],
     "ss12": ["RAMCRC_SYNC_STAGE_KIB=12"],
     "spf0": ["RAMCRC_SYNC_PF=0"],
-    "searly": ["RAMCRC_SYNC_EARLY=1"],
     "sstrict0": ["RAMCRC_SYNC_STRICT=0"],
     "ps15": ["RAMCRC_PART_SHIFT=15"],
     "ps17": ["RAMCRC_PART_SHIFT=17"],
@@ -48,10 +50,6 @@ VARIANTS = {
     # k_entries ping-pong depth / waves per CU
     "pu4": ["RAMCRC_PU=4"],
     "ew8": ["RAMCRC_ENT_WAVES=8"],
-    # long-phase probes (WRONG results, A/B timing only)
-    "pfold0": ["RAMCRC_PROBE_FOLD=1"],
-    "pfoldcf": ["RAMCRC_PROBE_FOLD=2"],
-    "pmask": ["RAMCRC_PROBE_MASK=1"],
     "pu3": ["RAMCRC_PU=3"],
     # k_entries phase stamps (tools/stamps.py)
     "stamps": ["RAMCRC_STAMPS=1"],
@@ -61,15 +59,12 @@ VARIANTS = {
     "sk50": ["RAMCRC_AGE_SKEW=50"],
     "oc2": ["RAMCRC_OCTET_COST=2"],
     "sk80": ["RAMCRC_AGE_SKEW=80"],
-    "ss7": ["RAMCRC_SYNC_STAGE_KIB=7"],
     "ss9": ["RAMCRC_SYNC_STAGE_KIB=9"],
     "fw8": ["RAMCRC_FIX_WIN_KIB=8"],
-    "sh5_ss7": ["RAMCRC_SYNC_HOPS=5", "RAMCRC_SYNC_STAGE_KIB=7"],
     "oc6": ["RAMCRC_OCTET_COST=6"],
     "sk120": ["RAMCRC_AGE_SKEW=120"],
     "nobatch": ["RAMCRC_STEP_BATCH=0"],
     # round 4: long-phase age skew re-tune (k_entries share per wave by age rank)
-    "sk0": ["RAMCRC_AGE_SKEW=0"],
     "sk60": ["RAMCRC_AGE_SKEW=60"],
     "sk100": ["RAMCRC_AGE_SKEW=100"],
     "sk180": ["RAMCRC_AGE_SKEW=180"],
@@ -78,8 +73,6 @@ VARIANTS = {
     "tk5": ["RAMCRC_TINY_K=5"],
     "tk6": ["RAMCRC_TINY_K=6"],
     "bo0": ["RAMCRC_BIN_ONE=0"],
-    # round 5: the guarded scatter after k_bin_one (A/B of its cost only; 0 is unsafe)
-    "rs0": ["RAMCRC_BIN_RESCUE=0"],
     # round 5: tiny tables built in LDS from basis words (0 = copied from g_tab)
     "tg0": ["RAMCRC_TINY_GEN=0"],
     "hm0": ["RAMCRC_TINY_HM=0"],

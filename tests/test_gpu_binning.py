@@ -311,14 +311,15 @@ def test_concurrent_contexts_config3(ramcrc, oracle_mod):
             c.close()
 
 
-def test_long_phase_steals_on_sparse_batches(ctx, oracle_mod):
-    """Batches of a few long entries (0.5-60 KiB) among tiny ones: most of
-    k_entries' 256 workgroups own no octet of the long phase and steal from
-    the few that do, so deques are drained, over-drained by failing steals
-    and raced on.  Every CRC must still be exact, with and without initial
-    states, over many batches on one context (the round-5 deque bug -- an
-    over-drained back wrapping below the front -- claimed octets past the
-    table)."""
+def test_long_phase_sparse_batches(ctx, oracle_mod):
+    """Batches of a few long entries (0.5-60 KiB) among tiny ones: the long
+    phase's static age-weighted shares (k_entries) then give
+    most workgroups and waves an empty or partial range, and the role split
+    sends most workgroups to the tiny phase.  Every CRC must be exact, with
+    and without initial states, over many batches on one context.  (Written
+    for round 5's work-stealing deques, whose failing steal once claimed
+    octets past the table; the static shares that replaced them keep the
+    same edge cases.)"""
     rng = np.random.default_rng(77)
     total = 8 << 20
     host = oracle_mod.splitmix_bytes(5, total)

@@ -277,3 +277,21 @@ def test_stream_host_config5_8mib(ctx, oracle_mod):
     assert np.array_equal(got, want)
     got = ctx.stream_host(host, seg, 61, batch=8, depth=2)
     assert np.array_equal(got, want[:61])
+
+
+def test_unknown_flag_bits_refused(ctx, ramcrc):
+    """Flag bits other than RAMCRC_FINALIZE are EINVAL (2 was round 4's
+    RAMCRC_ORDERED, removed; include/ramcrc.h RAMCRC_ABI_VERSION)."""
+    import ctypes
+    L = ramcrc.lib()
+    data = torch.zeros(1024, dtype=torch.uint8, device="cuda")
+    off = dev(np.array([0, 100], dtype=np.int64))
+    ln = dev(np.array([100, 200], dtype=np.int64))
+    out = torch.zeros(2, dtype=torch.int32, device="cuda")
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    for fl in (2, 4, 0x80000000):
+        assert L.ramcrc_batch_device(ctx._h, p(data), p(off), p(ln), None, p(out), 2, fl, None) == -1
+        assert L.ramcrc_entries_device(ctx._h, p(data), p(off), p(ln), None, p(out), 2, fl, None) == -1
+        assert L.ramcrc_segments_device(ctx._h, p(data), 512, 2, None, p(out), fl, None) == -1
+    assert L.ramcrc_batch_device(ctx._h, p(data), p(off), p(ln), None, p(out), 2, 1, None) == 0
+    torch.cuda.synchronize()
