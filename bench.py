@@ -654,6 +654,31 @@ def replay_cpu_baseline(host, seg_bytes, certs, nsample, reps=3):
             "all_verified": failed == 0}
 
 
+def replay_bit_exact(host, seg_bytes, certs, ns, table, obj_crc):
+    """The GPU's walk records and object CRCs of the first ns segments against
+    the oracle: records = the restated Segment::checkMetadataIntegrity walk
+    (src/Segment.cc:758-800) of each segment, CRCs = the restated
+    Object::computeChecksum (src/Object.cc:805-819) of those records."""
+    from oracle import oracle
+    certs = np.ascontiguousarray(certs, dtype=np.uint32).reshape(-1, 2)
+    table = np.ascontiguousarray(table, dtype=np.uint32).reshape(-1, 4)
+    mine = table[:, 0] < ns
+    g_tab, g_crc = table[mine], obj_crc[mine]
+    order = np.lexsort((g_tab[:, 1], g_tab[:, 0]))
+    g_tab, g_crc = g_tab[order], g_crc[order]
+    want = []
+    for s in range(ns):
+        _, _, _, t = oracle.check_metadata(host[s * seg_bytes:(s + 1) * seg_bytes], int(certs[s, 0]),
+                                           int(certs[s, 1]), segment=s, capacity=seg_bytes)
+        want.append(t)
+    want = np.concatenate(want) if want else np.zeros((0, 4), np.uint32)
+    records_ok = bool(np.array_equal(g_tab, want))
+    _, crc, _ = oracle.verify_objects(host[:ns * seg_bytes], seg_bytes, want, ns)
+    crcs_ok = records_ok and bool(np.array_equal(g_crc, crc))
+    return {"segments": ns, "records": int(want.shape[0]), "records_match": records_ok,
+            "object_crcs_match": crcs_ok}
+
+
 def _walk_cu_list(ncu, walk_cus):
     """CUs for the walk stream: runs of 8 consecutive CU ids spread evenly
     over the device, so every XCD gets an equal share whether CU ids map to
@@ -779,10 +804,16 @@ def run_replay(args, ranks):
                          and np.array_equal(status[:, 2], counts)
                          and np.array_equal(status[:, 1], certs[:, 1]))
     obj_bytes = int(counts.sum()) * (segments.OBJECT_OVERHEAD + args.value_len - 4)
-    cpu = None
+    cpu, exact = None, None
     if not args.no_cpu_baseline:
         ns = min(args.replay_cpu_sample, nseg)
-        cpu = replay_cpu_baseline(d[:ns * seg].cpu().numpy(), seg, certs, ns)
+        sample = d[:ns * seg].cpu().numpy()
+        cpu = replay_cpu_baseline(sample, seg, certs, ns)
+        if not args.walk_cus:
+            n = int(rv.n_entries.item())
+            exact = replay_bit_exact(sample, seg, certs, ns, rv.entries[:n].cpu().numpy().view(np.uint32),
+                                     rv.obj_crc[:n].cpu().numpy().view(np.uint32))
+            cpu["bit_exact_vs_gpu"] = exact["object_crcs_match"]
     ctx.close()
     scan_s = scan_ms / args.steps / 1e3
     achieved = obj_bytes / scan_s / 1e9 if scan_s > 0 else None
@@ -813,6 +844,138 @@ def run_replay(args, ranks):
                      "algorithmic_bytes_per_launch": obj_bytes, "traffic_key": tkey},
         "cpu_baseline": cpu,
         "all_segments_verified": ok,
+        "bit_exact": None if exact is None else exact["object_crcs_match"],
+        "bit_exact_check": exact,
+    }
+
+
+def run_contexts(args, ranks):
+    """The reference's concurrency shape on one GPU: K replay (or log-entry)
+    threads, as RecoverSegmentBenchmark sweeps replay threads {1, 2, 4, 8, 16}
+    (nanobenchmarks/RecoverSegmentBenchmark.cc:181-183,273).  Each host thread
+    owns one context and one stream (include/ramcrc.h: one context per
+    launching thread) and its own copy of the batch, and submits a step per
+    iteration back to back while the others run.  value = K x batch bytes x
+    steps / wall time.  Every output of every context is checked: entries
+    against the reference's intelCrc32C per entry, replay statuses and object
+    CRCs against context 0's and context 0's first segments against the
+    oracle's walk and checksums.  bin_rescues: k_bin_one launches of each
+    context that aborted (grid not all resident in time) and were binned by
+    the guarded scatter."""
+    import threading
+    import torch
+    from ramcloud_amd import ramcrc, segments, workloads
+    K = args.contexts
+    dev = ranks.local
+    ctxs = [ramcrc.Context(dev) for _ in range(K)]
+    streams = [torch.cuda.Stream() for _ in range(K)]
+    if args.config == "entries":
+        lens = workloads.entry_lengths(args.entries)
+        if args.entry_size:
+            lens = lens * 0 + np.uint64(args.entry_size)
+        offs = workloads.packed_offsets(lens)
+        total = int(lens.sum())
+        host = workloads.splitmix_bytes_np(workloads.ENTRY_SEED, total)
+        data0 = torch.from_numpy(host).cuda()
+        off_t = torch.from_numpy(offs.view(np.int64)).cuda()
+        len_t = torch.from_numpy(lens.view(np.int64)).cuda()
+        datas = [data0] + [data0.clone() for _ in range(K - 1)]
+        outs = [torch.zeros(lens.size, dtype=torch.int32, device="cuda") for _ in range(K)]
+        step_bytes = total
+
+        def step(i):
+            ctxs[i].entries(datas[i], off_t, len_t, outs[i], stream=streams[i])
+        what = f"{lens.size} log entries ({'fixed %d B' % args.entry_size if args.entry_size else '100B/1KiB/4KiB Zipf'})"
+    else:
+        seg = args.seg_mib * MiB
+        nseg = args.replay_nseg
+        d0 = torch.empty(nseg * seg, dtype=torch.uint8, device="cuda")
+        certs_t = torch.zeros((nseg, 2), dtype=torch.int32, device="cuda")
+        per, _, _ = _fill_recovery_shard(ctxs[0], d0, seg, 0, nseg, args.value_len, certs=certs_t)
+        certs = certs_t.cpu().numpy().view(np.uint32)
+        cap = per * nseg + nseg
+        datas = [d0] + [d0.clone() for _ in range(K - 1)]
+        rvs = [segments.RecoveryVerify(ctxs[i], nseg, seg, entries_cap=cap) for i in range(K)]
+        step_bytes = nseg * seg
+        sts = [None] * K
+
+        def step(i):
+            sts[i] = rvs[i].verify(datas[i], certs_t, stream=streams[i])
+        what = f"{nseg} x {args.seg_mib} MiB segments of {args.value_len} B-value objects (replay verify)"
+    torch.cuda.synchronize()
+    go = threading.Barrier(K + 1)
+    done = threading.Barrier(K + 1)
+    errors = []
+
+    def worker(i):
+        try:
+            torch.cuda.set_device(dev)
+            for _ in range(args.warmup):
+                step(i)
+            streams[i].synchronize()
+        except Exception as e:   # reported below; the barriers still release
+            errors.append(repr(e))
+        go.wait()
+        try:
+            for _ in range(args.steps):
+                step(i)
+            streams[i].synchronize()
+        except Exception as e:
+            errors.append(repr(e))
+        done.wait()
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(K)]
+    for t in th:
+        t.start()
+    go.wait()
+    t0 = time.perf_counter()
+    done.wait()
+    elapsed = time.perf_counter() - t0
+    for t in th:
+        t.join()
+    torch.cuda.synchronize()
+    if errors:
+        raise RuntimeError(f"context threads failed: {errors[:3]}")
+    for c in ctxs:
+        c.check()
+    rescues = [c.bin_rescues() for c in ctxs]
+    check = {}
+    if args.config == "entries":
+        from oracle import oracle
+        want = (oracle.ref_entries(host, offs, lens, threads=baseline_threads(host_cpu_info()))
+                if oracle.ref_available() else oracle.entries(host, offs, lens))
+        check["all_crcs_match"] = all(
+            bool(np.array_equal(o.cpu().numpy().view(np.uint32), want)) for o in outs)
+        check["crcs_checked"] = int(lens.size) * K
+    else:
+        ok = True
+        n0 = int(rvs[0].n_entries.item())
+        crc0 = rvs[0].obj_crc[:n0].cpu().numpy()
+        tab0 = rvs[0].entries[:n0].cpu().numpy()
+        for i in range(K):
+            st = sts[i].cpu().numpy().view(np.uint32)
+            ok = ok and bool((st[:, 0] == segments.SEG_OK).all() and (st[:, 3] == 0).all()
+                             and (st[:, 2] == per).all() and np.array_equal(st[:, 1], certs[:, 1]))
+            if i:
+                n = int(rvs[i].n_entries.item())
+                ok = ok and n == n0 and np.array_equal(rvs[i].obj_crc[:n].cpu().numpy(), crc0) \
+                    and np.array_equal(rvs[i].entries[:n].cpu().numpy(), tab0)
+        ns = min(8, nseg)
+        ex = replay_bit_exact(datas[0][:ns * seg].cpu().numpy(), seg, certs, ns,
+                              tab0.view(np.uint32), crc0.view(np.uint32))
+        check = {"all_contexts_equal_and_verified": ok, "oracle_sample": ex,
+                 "all_crcs_match": ok and ex["object_crcs_match"], "crcs_checked": n0 * K}
+    for c in ctxs:
+        c.close()
+    return {
+        "metric": f"aggregate device-resident CRC32C GB/s, {K} concurrent contexts on one GPU: {what}",
+        "value": round(K * step_bytes * args.steps / elapsed / 1e9, 2), "unit": "GB/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": what, "contexts": K, "threads": K,
+                   "per_context": "own context, stream and copy of the batch; steps back to back"},
+        "bin_rescues": rescues, "check": check, "bit_exact": check["all_crcs_match"],
     }
 
 
@@ -959,6 +1122,9 @@ def parse_args(argv=None):
                          "(a multiple of 8) beside the object scan on the rest; 0 = serial")
     ap.add_argument("--serial-walk", action="store_true",
                     help="replay config: one wavefront per segment walk (RAMCRC_OPT_SERIAL_WALK)")
+    ap.add_argument("--contexts", type=int, default=0,
+                    help="entries / replay config: K host threads, one context and stream each, "
+                         "submitting concurrently (RecoverSegmentBenchmark's replay threads)")
     ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-t1", action="store_true", help="config 4 at N>1: skip the 1-GPU t1 run")
@@ -1013,6 +1179,8 @@ def main():
             config = "c2" if ranks.world == 1 else "recovery"
         run = {"c2": run_c2, "recovery": run_recovery, "entries": run_entries,
                "replay": run_replay, "append": run_append, "stream": run_stream}[config]
+        if args.contexts and config in ("entries", "replay"):
+            run = run_contexts
         line = run(args, ranks)
     if ranks.rank == 0:
         emit(line)
