@@ -948,21 +948,26 @@ def run_contexts(args, ranks):
             bool(np.array_equal(o.cpu().numpy().view(np.uint32), want)) for o in outs)
         check["crcs_checked"] = int(lens.size) * K
     else:
+        # segments take their record slots in the order their walks finish,
+        # so tables are compared in (segment, offset) order
+        def canon(rv):
+            n = int(rv.n_entries.item())
+            tab = rv.entries[:n].cpu().numpy().view(np.uint32)
+            crc = rv.obj_crc[:n].cpu().numpy().view(np.uint32)
+            o = np.lexsort((tab[:, 1], tab[:, 0]))
+            return tab[o], crc[o]
         ok = True
-        n0 = int(rvs[0].n_entries.item())
-        crc0 = rvs[0].obj_crc[:n0].cpu().numpy()
-        tab0 = rvs[0].entries[:n0].cpu().numpy()
+        tab0, crc0 = canon(rvs[0])
+        n0 = tab0.shape[0]
         for i in range(K):
             st = sts[i].cpu().numpy().view(np.uint32)
             ok = ok and bool((st[:, 0] == segments.SEG_OK).all() and (st[:, 3] == 0).all()
                              and (st[:, 2] == per).all() and np.array_equal(st[:, 1], certs[:, 1]))
             if i:
-                n = int(rvs[i].n_entries.item())
-                ok = ok and n == n0 and np.array_equal(rvs[i].obj_crc[:n].cpu().numpy(), crc0) \
-                    and np.array_equal(rvs[i].entries[:n].cpu().numpy(), tab0)
+                tab, crc = canon(rvs[i])
+                ok = ok and np.array_equal(tab, tab0) and np.array_equal(crc, crc0)
         ns = min(8, nseg)
-        ex = replay_bit_exact(datas[0][:ns * seg].cpu().numpy(), seg, certs, ns,
-                              tab0.view(np.uint32), crc0.view(np.uint32))
+        ex = replay_bit_exact(datas[0][:ns * seg].cpu().numpy(), seg, certs, ns, tab0, crc0)
         check = {"all_contexts_equal_and_verified": ok, "oracle_sample": ex,
                  "all_crcs_match": ok and ex["object_crcs_match"], "crcs_checked": n0 * K}
     for c in ctxs:

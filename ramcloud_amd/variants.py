@@ -97,4 +97,6 @@ VARIANTS = {
     "kap288": ["RAMCRC_SPLIT_KAPPA=288"],
     "bsp32": ["RAMCRC_BIN_SLEEP=32"],
     "cpf0": ["RAMCRC_COUNT_PF=0"],
+    # round 6: the speculative direct tiny pass off
+    "spec0": ["RAMCRC_SPEC_TINY=0"],
 }
