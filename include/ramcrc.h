@@ -455,6 +455,14 @@ int ramcrc_assemble_objects_host(ramcrc_ctx* ctx, void* const* objs, const uint6
  *                           is not such a one the binning behind it runs as
  *                           usual.  Results are identical in every mode. */
 #define RAMCRC_OPT_SPEC_TINY 6
+/*   RAMCRC_OPT_VERIFY_IN_WALK  ramcrc_replay_verify_device with small entries
+ *                           (the objects of 64- and 128-byte values): 1
+ *                           (default) checks each object while its record is
+ *                           copied, from the object bytes staged in LDS, and
+ *                           skips the binned object scan; 2 does so for every
+ *                           batch; 0 always runs the binned scan.  Identical
+ *                           results. */
+#define RAMCRC_OPT_VERIFY_IN_WALK 7
 int ramcrc_ctx_set_option(ramcrc_ctx* ctx, int option, int64_t value);
 
 /* Kernel timing (for benchmarks): when enabled, every launch brackets its

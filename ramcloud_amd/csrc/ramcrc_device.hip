@@ -229,6 +229,7 @@ int ramcrc_ctx_destroy(ramcrc_ctx* c)
     if (c->walk_blocks) (void)hipFree(c->walk_blocks);
     if (c->walk_pool_used) (void)hipFree(c->walk_pool_used);
     if (c->walk_sum) (void)hipFree(c->walk_sum);
+    if (c->walk_left) (void)hipFree(c->walk_left);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->spec_hint) (void)hipHostFree(c->spec_hint);
@@ -279,6 +280,11 @@ int ramcrc_ctx_set_option(ramcrc_ctx* c, int option, int64_t value)
         if (value < 0 || value > 2)
             return RAMCRC_EINVAL;
         c->spec_tiny = int(value);
+        return RAMCRC_OK;
+    case RAMCRC_OPT_VERIFY_IN_WALK:
+        if (value < 0 || value > 2)
+            return RAMCRC_EINVAL;
+        c->verify_in_walk = int(value);
         return RAMCRC_OK;
     case RAMCRC_OPT_WALK_PART_SHIFT:
         if (value != 0 && (value < kPartShiftMin || value > 20))
@@ -676,10 +682,11 @@ namespace {
 int walk_impl(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride, uint32_t seg_capacity,
               uint64_t n_seg, const ramcrc_seg_cert* d_certs, ramcrc_seg_status* d_status,
               ramcrc_seg_entry* d_entries, uint64_t entries_cap, uint64_t* d_n_entries,
-              hipStream_t s, uint32_t* sum);
+              hipStream_t s, uint32_t* sum, uint32_t* d_obj_crc = nullptr);
 int verify_impl(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride,
                 const ramcrc_seg_entry* d_entries, uint64_t entries_cap, const uint64_t* d_n_entries,
-                uint32_t* d_obj_crc, ramcrc_seg_status* d_status, hipStream_t s, const uint32_t* sum);
+                uint32_t* d_obj_crc, ramcrc_seg_status* d_status, hipStream_t s, const uint32_t* sum,
+                uint64_t n_seg = 0);
 }  // namespace
 
 int ramcrc_segment_walk_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride,
@@ -713,18 +720,19 @@ int ramcrc_replay_verify_device(ramcrc_ctx* c, const void* d_base, uint64_t seg_
     if (rc)
         return rc;
     rc = walk_impl(c, d_base, seg_stride, seg_capacity, n_seg, d_certs, d_status, d_entries,
-                   entries_cap, d_n_entries, s, c->walk_sum);
+                   entries_cap, d_n_entries, s, c->walk_sum,
+                   entries_cap && c->verify_in_walk ? d_obj_crc : nullptr);
     if (rc || n_seg == 0)
         return rc;
     return verify_impl(c, d_base, seg_stride, d_entries, entries_cap, d_n_entries, d_obj_crc,
-                       d_status, s, c->walk_sum);
+                       d_status, s, c->walk_sum, n_seg);
 }
 
 namespace {
 int walk_impl(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride, uint32_t seg_capacity,
               uint64_t n_seg, const ramcrc_seg_cert* d_certs, ramcrc_seg_status* d_status,
               ramcrc_seg_entry* d_entries, uint64_t entries_cap, uint64_t* d_n_entries,
-              hipStream_t s, uint32_t* sum)
+              hipStream_t s, uint32_t* sum, uint32_t* d_obj_crc)
 {
     if (!d_n_entries || (entries_cap && !d_entries))
         return RAMCRC_EINVAL;
@@ -794,8 +802,13 @@ int walk_impl(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride, uint32_t s
             rc = grow_device(reinterpret_cast<void**>(&c->walk_blocks), &c->walk_blocks_cap,
                              total * kMaxBlocks, sizeof(uint32_t));
         if (!rc)
-            rc = grow_device(reinterpret_cast<void**>(&c->walk_pool_used), &c->walk_pool_used_cap, 2,
-                             sizeof(unsigned long long));   // [1]: the part shift word
+            rc = grow_device(reinterpret_cast<void**>(&c->walk_pool_used), &c->walk_pool_used_cap, 3,
+                             sizeof(unsigned long long));   // [1]: the part shift word, [2]: k_left's count
+        // verify-in-walk mode (fused call): the list of records k_left checks
+        const uint64_t left_cap = entries_cap / 8 + 65536 < entries_cap ? entries_cap / 8 + 65536 : entries_cap;
+        if (!rc && d_obj_crc && sum)
+            rc = grow_device(reinterpret_cast<void**>(&c->walk_left), &c->walk_left_cap, left_cap,
+                             sizeof(uint32_t));
         if (rc)
             return rc;
         PWalk pw{};
@@ -822,6 +835,13 @@ int walk_impl(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride, uint32_t s
         pw.pool_used = c->walk_pool_used;
         pw.pool_cap = pool_blocks;
         pw.sum = sum;
+        if (d_obj_crc && sum) {
+            pw.obj_crc = d_obj_crc;
+            pw.left = c->walk_left;
+            pw.nleft = c->walk_pool_used + 2;
+            pw.left_cap = left_cap;
+            pw.vmode = uint32_t(c->verify_in_walk);
+        }
         hipLaunchKernelGGL(k_walk_probe, dim3(1), dim3(kWaveSize), 0, s, pw, c->walk_pshift, geo);
         HIPCHK(hipGetLastError());
         if (nparts > 1) {
@@ -842,6 +862,13 @@ int walk_impl(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride, uint32_t s
             gc = uint64_t(32) * c->ncu;
         hipLaunchKernelGGL(k_walk_copy, dim3(gc), dim3(256), 0, s, pw);
         HIPCHK(hipGetLastError());
+        if (pw.obj_crc) {   // verify-in-walk mode, decided by k_walk_probe (else it exits)
+            uint64_t gv = (total + pool_blocks + kVWaves - 1) / kVWaves;
+            if (gv > uint64_t(16) * c->ncu)
+                gv = uint64_t(16) * c->ncu;
+            hipLaunchKernelGGL(k_walk_copyv, dim3(gv), dim3(kVWaves * kWaveSize), 0, s, pw);
+            HIPCHK(hipGetLastError());
+        }
         w.only = c->walk_fallback;
     }
     hipLaunchKernelGGL(k_seg_walk, dim3(grid), dim3(kWaveSize), 0, s, w);
@@ -900,7 +927,8 @@ int ramcrc_verify_objects_device(ramcrc_ctx* c, const void* d_base, uint64_t seg
 namespace {
 int verify_impl(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride,
                 const ramcrc_seg_entry* d_entries, uint64_t entries_cap, const uint64_t* d_n_entries,
-                uint32_t* d_obj_crc, ramcrc_seg_status* d_status, hipStream_t s, const uint32_t* sum)
+                uint32_t* d_obj_crc, ramcrc_seg_status* d_status, hipStream_t s, const uint32_t* sum,
+                uint64_t n_seg)
 {
     if (entries_cap == 0)
         return RAMCRC_OK;
@@ -920,6 +948,14 @@ int verify_impl(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride,
     d.seg_status = reinterpret_cast<const u32x4*>(d_status);
     d.out = d_obj_crc;
     d.flags = RAMCRC_FINALIZE;
+    if (sum && c->walk_left && !c->serial_walk) {
+        // the fused call's verify-in-walk leftovers (exits unless k_walk_probe chose that mode)
+        uint64_t gl = uint64_t(4) * c->ncu;
+        hipLaunchKernelGGL(k_left, dim3(gl), dim3(256), 0, s, d, d_status, sum, c->walk_left,
+                           reinterpret_cast<const unsigned long long*>(c->walk_pool_used + 2),
+                           c->walk_left_cap, n_seg);
+        HIPCHK(hipGetLastError());
+    }
     const uint32_t* nother = nullptr;
     rc = launch_planned<kRecords>(c, d, s, &nother, sum);
     if (rc)

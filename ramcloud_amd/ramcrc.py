@@ -35,6 +35,7 @@ OPT_TEST_FAIL_AFTER_COUNT = 3
 OPT_TEST_DIRTY_BINS = 4
 OPT_TEST_BIN_STRAGGLER = 5
 OPT_SPEC_TINY = 6
+OPT_VERIFY_IN_WALK = 7
 
 
 class RamcrcError(RuntimeError):

@@ -53,6 +53,7 @@ def test_fused_equals_split_small_values(ramcrc):
     from ramcloud_amd import segments
     nseg, vlen = 16, 64
     ctx = ramcrc.Context(0)
+    ctx.set_option(ramcrc.OPT_VERIFY_IN_WALK, 0)   # the binned verify's direct tiny path
     try:
         d, certs, per, ck = _batch(ramcrc, ctx, nseg, vlen)
         eb = segments.entry_bytes(vlen)
@@ -113,6 +114,7 @@ def test_fused_multi_window_direct(ramcrc, vlen):
     from ramcloud_amd import segments
     nseg = 12
     ctx = ramcrc.Context(0)
+    ctx.set_option(ramcrc.OPT_VERIFY_IN_WALK, 0)   # the binned verify's direct multi-window path
     try:
         d, certs, per, ck = _batch(ramcrc, ctx, nseg, vlen, first_seed=0x1281 + vlen)
         eb = segments.entry_bytes(vlen)
@@ -133,3 +135,114 @@ def test_fused_multi_window_direct(ramcrc, vlen):
         assert fs[7, 0] & segments.SEG_BAD_CHECKSUM and not fs[7, 0] & segments.SEG_OK
     finally:
         ctx.close()
+
+
+def _hist_empty(ctx, n):
+    """The verify-in-walk mode was taken: the binned verify's count pass
+    exited with an empty histogram although the table holds n records."""
+    _, _, hist, par_next = ctx.debug_bins()
+    return n > 0 and int(hist[par_next ^ 1].sum()) == 0
+
+
+@pytest.mark.parametrize("vlen", [64, 128, 160])
+def test_verify_in_walk_small_values(ramcrc, vlen):
+    """Verify in the walk (RAMCRC_OPT_VERIFY_IN_WALK, the default for small
+    entries): k_walk_copyv checks every object from LDS while it copies the
+    records, and the binned scan has nothing left.  RecoverSegmentBenchmark
+    segments with a damaged object value, a damaged stored checksum and a
+    damaged certificate; status words, record table and object CRCs equal to
+    the split calls' (which bin and scan)."""
+    from ramcloud_amd import segments
+    nseg = 12
+    ctx = ramcrc.Context(0)
+    try:
+        d, certs, per, ck = _batch(ramcrc, ctx, nseg, vlen, first_seed=0xF00D + vlen)
+        eb = segments.entry_bytes(vlen)
+        d[1 * SEG + 77 * eb + eb - 2] ^= 0x10           # a value byte
+        d[6 * SEG + 5000 * eb + 2 + 1] ^= 0x01          # the stored checksum (payload byte 1)
+        certs[9, 1] ^= 0x4000                           # the whole segment fails
+        cap = nseg * per + 1024
+        fs, fn, ft, fc = _run(ramcrc, ctx, d, certs, nseg, cap, fused=True)
+        assert _hist_empty(ctx, fn)
+        ss, sn, st, sc = _run(ramcrc, ctx, d, certs, nseg, cap, fused=False)
+        assert fn == sn == nseg * per
+        assert np.array_equal(fs, ss)
+        assert np.array_equal(ft, st)
+        assert np.array_equal(fc, sc)
+        bad = np.zeros(nseg, np.uint32)
+        bad[1] = bad[6] = 1
+        assert np.array_equal(fs[:, 3], bad)
+        assert fs[9, 0] & segments.SEG_BAD_CHECKSUM and not fs[9, 0] & segments.SEG_OK
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("seed", [4242, 17])
+def test_verify_in_walk_forced_mixed(ramcrc, oracle_mod, seed):
+    """The verify-in-walk mode forced (2) on segments of every entry kind
+    (objects of 24 B .. 200 KiB, tombstones, safe versions; junk headers in
+    the payloads, so parts are misguessed and records are written by the
+    fix-up's re-walks): objects too long for the stage or the leftover list
+    send the whole table to the binned verify (kHardFull), the other types go
+    to k_left.  One damaged entry.  Equal to the split calls and to the
+    oracle."""
+    import segment_cases
+    cap, nseg = 1 << 20, 8
+    buf, certs, counts = segment_cases.mixed_segments(oracle_mod, nseg, cap, seed=seed)
+    buf[3 * cap + cap // 2] ^= 0x20
+    d = torch.from_numpy(buf).cuda()
+    dc = torch.from_numpy(certs.view(np.int32)).cuda()
+    exp_status, exp_table, exp_crc = segment_cases.oracle_walk(oracle_mod, buf, certs, nseg, cap=cap)
+    from ramcloud_amd import segments
+    got = {}
+    for mode in (2, 0):
+        ctx = ramcrc.Context(0)
+        try:
+            ctx.set_option(ramcrc.OPT_VERIFY_IN_WALK, mode)
+            rv = segments.RecoveryVerify(ctx, nseg, cap, entries_cap=int(counts.sum()) + 4096)
+            st = rv.verify(d, dc, check=True)
+            torch.cuda.synchronize()
+            n = int(rv.n_entries.item())
+            table = rv.entries[:n].cpu().numpy().view(np.uint32)
+            crc = rv.obj_crc[:n].cpu().numpy().view(np.uint32)
+            o = np.lexsort((table[:, 1], table[:, 0]))
+            got[mode] = (st.cpu().numpy().view(np.uint32).copy(), table[o], crc[o])
+        finally:
+            ctx.close()
+    for k in range(3):
+        assert np.array_equal(got[2][k], got[0][k]), k
+    assert np.array_equal(got[2][0], exp_status)
+    assert np.array_equal(got[2][1], exp_table)
+    mask = segment_cases.replay_crc_mask(buf, cap, exp_table)
+    assert np.array_equal(got[2][2][mask], exp_crc[mask])
+
+
+def test_verify_in_walk_replay_mix(ramcrc, oracle_mod, golden):
+    """The replay mix (objects, tombstones, safe versions, prepared ops and
+    their tombstones, decision records, participant lists; valid and damaged)
+    with the verify-in-walk mode forced: the other types go through k_left.
+    Equal to the split calls."""
+    import segment_cases
+    buf, certs, bad_exp, _ = segment_cases.build_replay_mix(oracle_mod, golden)
+    nseg, cap = certs.shape[0], segment_cases.CAPACITY
+    d = torch.from_numpy(buf).cuda()
+    dc = torch.from_numpy(np.ascontiguousarray(certs).view(np.int32)).cuda()
+    from ramcloud_amd import segments
+    got = {}
+    for mode in (2, 0):
+        ctx = ramcrc.Context(0)
+        try:
+            ctx.set_option(ramcrc.OPT_VERIFY_IN_WALK, mode)
+            rv = segments.RecoveryVerify(ctx, nseg, cap, entries_cap=nseg * (cap // 14 + 1))
+            st = rv.verify(d, dc, check=True)
+            torch.cuda.synchronize()
+            n = int(rv.n_entries.item())
+            table = rv.entries[:n].cpu().numpy().view(np.uint32)
+            crc = rv.obj_crc[:n].cpu().numpy().view(np.uint32)
+            o = np.lexsort((table[:, 1], table[:, 0]))
+            got[mode] = (st.cpu().numpy().view(np.uint32).copy(), table[o], crc[o])
+        finally:
+            ctx.close()
+    for k in range(3):
+        assert np.array_equal(got[2][k], got[0][k]), k
+    assert np.array_equal(got[2][0][:, 3], bad_exp) and int(bad_exp.sum()) > 0
