@@ -768,6 +768,7 @@ def run_replay(args, ranks):
     import torch
     from ramcloud_amd import ramcrc, segments
     ctx = ramcrc.Context(ranks.local)
+    ctx.set_option(ramcrc.OPT_VERIFY_IN_WALK, args.verify_in_walk)
     if args.serial_walk:
         ctx.set_serial_walk(True)
     if args.walk_part_shift:
@@ -830,6 +831,7 @@ def run_replay(args, ranks):
                                f"{args.value_len} B-value objects",
                    "pipeline": (f"walk on {args.walk_cus} CUs beside the scan of the previous batch"
                                 if args.walk_cus else "none"),
+                   "verify_in_walk": args.verify_in_walk,
                    "walk": ("serial (one wave per segment)" if args.serial_walk else
                             f"parallel ({1 << (args.walk_part_shift - 10)} KiB parts, forced)"
                             if args.walk_part_shift else
@@ -868,6 +870,8 @@ def run_contexts(args, ranks):
     K = args.contexts
     dev = ranks.local
     ctxs = [ramcrc.Context(dev) for _ in range(K)]
+    for c in ctxs:
+        c.set_option(ramcrc.OPT_VERIFY_IN_WALK, args.verify_in_walk)
     streams = [torch.cuda.Stream() for _ in range(K)]
     if args.config == "entries":
         lens = workloads.entry_lengths(args.entries)
@@ -1125,6 +1129,9 @@ def parse_args(argv=None):
     ap.add_argument("--walk-cus", type=int, default=0,
                     help="replay config: pipeline batches, walking on this many CUs "
                          "(a multiple of 8) beside the object scan on the rest; 0 = serial")
+    ap.add_argument("--verify-in-walk", type=int, default=1, choices=[0, 1, 2],
+                    help="replay: check small objects while the walk copies their records "
+                         "(RAMCRC_OPT_VERIFY_IN_WALK; 1 = for small entries, the default)")
     ap.add_argument("--serial-walk", action="store_true",
                     help="replay config: one wavefront per segment walk (RAMCRC_OPT_SERIAL_WALK)")
     ap.add_argument("--contexts", type=int, default=0,
