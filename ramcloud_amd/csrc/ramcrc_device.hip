@@ -863,7 +863,7 @@ int walk_impl(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride, uint32_t s
         hipLaunchKernelGGL(k_walk_copy, dim3(gc), dim3(256), 0, s, pw);
         HIPCHK(hipGetLastError());
         if (pw.obj_crc) {   // verify-in-walk mode, decided by k_walk_probe (else it exits)
-            uint64_t gv = (total + pool_blocks + kVWaves - 1) / kVWaves;
+            uint64_t gv = (total + kVWaves - 1) / kVWaves;   // a wave per part
             if (gv > uint64_t(16) * c->ncu)
                 gv = uint64_t(16) * c->ncu;
             hipLaunchKernelGGL(k_walk_copyv, dim3(gv), dim3(kVWaves * kWaveSize), 0, s, pw);
