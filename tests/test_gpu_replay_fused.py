@@ -144,7 +144,7 @@ def _hist_empty(ctx, n):
     return n > 0 and int(hist[par_next ^ 1].sum()) == 0
 
 
-@pytest.mark.parametrize("vlen", [64, 128, 160])
+@pytest.mark.parametrize("vlen", [64, 100, 128])
 def test_verify_in_walk_small_values(ramcrc, vlen):
     """Verify in the walk (RAMCRC_OPT_VERIFY_IN_WALK, the default for small
     entries): k_walk_copyv checks every object from LDS while it copies the
