@@ -778,7 +778,7 @@ int walk_impl(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride, uint32_t s
         // part size: chosen per batch on the device by k_walk_probe from the
         // entry density (or forced, RAMCRC_OPT_WALK_PART_SHIFT); grids and
         // scratch are sized for the smallest part it may choose
-        const uint32_t pshift = c->walk_pshift ? c->walk_pshift : kPartShift;
+        const uint32_t pshift = c->walk_pshift ? c->walk_pshift : kPartShiftLow;
         const uint32_t nparts = uint32_t((uint64_t(seg_capacity) + (1ull << pshift) - 1) >> pshift);
         const uint64_t total = n_seg * uint64_t(nparts);
         int rc = grow_device(&c->walk_parts, &c->walk_parts_cap, total, sizeof(PartRes));

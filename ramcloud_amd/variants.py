@@ -99,4 +99,8 @@ VARIANTS = {
     "cpf0": ["RAMCRC_COUNT_PF=0"],
     # round 6: the speculative direct tiny pass off
     "spec0": ["RAMCRC_SPEC_TINY=0"],
+    # round 6: dense batches in 32 KiB parts, k_walk_parts keeping 32 records per lane in LDS
+    "dense15": ["RAMCRC_PART_SHIFT_DENSE=15", "RAMCRC_PART_LREC=32"],
+    "lrec32": ["RAMCRC_PART_LREC=32"],
+    "vf0": ["RAMCRC_VFAST=0"],
 }
