@@ -103,4 +103,7 @@ VARIANTS = {
     "dense15": ["RAMCRC_PART_SHIFT_DENSE=15", "RAMCRC_PART_LREC=32"],
     "lrec32": ["RAMCRC_PART_LREC=32"],
     "vf0": ["RAMCRC_VFAST=0"],
+    # round 6: k_walk_copyv's byte tables in 8 / 16 copies (fewer LDS bank conflicts)
+    "vrep8": ["RAMCRC_VREP=8", "RAMCRC_VWAVES=8"],
+    "vrep16": ["RAMCRC_VREP=16", "RAMCRC_VWAVES=6"],
 }
