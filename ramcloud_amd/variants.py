@@ -106,4 +106,8 @@ VARIANTS = {
     # round 6: k_walk_copyv's byte tables in 8 / 16 copies (fewer LDS bank conflicts)
     "vrep8": ["RAMCRC_VREP=8", "RAMCRC_VWAVES=8"],
     "vrep16": ["RAMCRC_VREP=16", "RAMCRC_VWAVES=6"],
+    # round 6: k_walk_copyv's CRC by VALU bit-matrix (1) or half tables, half VALU (2)
+    "vcrc1": ["RAMCRC_VCRC=1"],
+    "vcrc2": ["RAMCRC_VCRC=2"],
+    "vcrc2r8": ["RAMCRC_VCRC=2", "RAMCRC_VREP=8", "RAMCRC_VWAVES=8"],
 }
