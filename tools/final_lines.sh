@@ -19,6 +19,11 @@ for v in 64 128 256 512 1024 2048 8192; do
   timeout -k 10 200 python bench.py --config replay --value-len $v > "$OUT/replay_$v.json" 2> "$OUT/replay_$v.err" || exit 1
 done
 timeout -k 10 200 python bench.py --config replay > "$OUT/replay.json" 2> "$OUT/replay.err" || exit 1
+# the reference's concurrency shape (RecoverSegmentBenchmark's replay threads)
+for K in ${KS:-1 4 16}; do
+  timeout -k 10 300 python bench.py --config entries --contexts $K > "$OUT/ctx_entries_k$K.json" 2> "$OUT/ctx_entries_k$K.err" || exit 1
+  timeout -k 10 300 python bench.py --config replay --value-len 64 --contexts $K --steps 10 > "$OUT/ctx_replay64_k$K.json" 2> "$OUT/ctx_replay64_k$K.err" || exit 1
+done
 P="rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof"
 timeout -k 10 200 $P -o c2 -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > "$OUT/prof_c2.json" 2> "$OUT/prof_c2.err" || exit 1
 timeout -k 10 200 $P -o c3 -- python3 bench.py --config entries --steps 20 --no-cpu-baseline > "$OUT/prof_c3.json" 2> "$OUT/prof_c3.err" || exit 1

@@ -17,9 +17,12 @@ def main(paths):
         r = d.get("roofline") or {}
         c = d.get("cpu_baseline") or {}
         ok = c.get("bit_exact_vs_gpu", c.get("all_verified"))
+        if d.get("bit_exact") is not None:
+            ok = f"{ok}/{d.get('bit_exact')}"
         print(f"{p}: {d.get('value')} {d.get('unit')} step {d.get('ms_per_step')} ms "
               f"frac {r.get('frac')} kernel {r.get('avg_kernel_ms')} ms traffic {r.get('traffic')} | "
-              f"cpu {c.get('value')} {c.get('kind')} x{c.get('cores')} exact {ok}")
+              f"cpu {c.get('value')} {c.get('kind')} x{c.get('cores')} exact {ok}"
+              + (f" rescues {d['bin_rescues']}" if "bin_rescues" in d else ""))
 
 
 if __name__ == "__main__":
