@@ -101,6 +101,8 @@ VARIANTS = {
     "spec0": ["RAMCRC_SPEC_TINY=0"],
     # round 6: dense batches in 32 KiB parts, k_walk_parts keeping 32 records per lane in LDS
     "dense15": ["RAMCRC_PART_SHIFT_DENSE=15", "RAMCRC_PART_LREC=32"],
+    "dense15a": ["RAMCRC_PART_SHIFT_DENSE=15", "RAMCRC_PART_LREC=32", "RAMCRC_SYNC_ADAPT=1"],
+    "sada": ["RAMCRC_SYNC_ADAPT=1"],
     "lrec32": ["RAMCRC_PART_LREC=32"],
     "vf0": ["RAMCRC_VFAST=0"],
     # round 6: k_walk_copyv's byte tables in 8 / 16 copies (fewer LDS bank conflicts)
