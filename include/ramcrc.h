@@ -446,15 +446,12 @@ int ramcrc_assemble_objects_host(ramcrc_ctx* ctx, void* const* objs, const uint6
  *                           (no arrival for 30 us) and the launch complete
  *                           through the two-launch binning with exact results. */
 #define RAMCRC_OPT_TEST_BIN_STRAGGLER 5
-/*   RAMCRC_OPT_SPEC_TINY  the speculative direct tiny pass of small-entry
- *                           table batches (ramcrc_entries_device /
- *                           ramcrc_batch_device): 1 (default) when this
- *                           context's last such batch was all entries of one
- *                           128-byte window, 2 always, 0 never.  The pass
- *                           checksums the caller's table in place; if an entry
- *                           is not such a one the binning behind it runs as
- *                           usual.  Results are identical in every mode. */
-#define RAMCRC_OPT_SPEC_TINY 6
+/*   RAMCRC_OPT_BIN_ONE     small-entry batches of at most one 4,096-entry
+ *                           tile per CU: 1 bins them with the one-launch
+ *                           k_bin_one (a grid-wide vote), 0
+ *                           (default since round 6) with the two-launch count
+ *                           and scatter.  Identical results. */
+#define RAMCRC_OPT_BIN_ONE 6
 /*   RAMCRC_OPT_VERIFY_IN_WALK  ramcrc_replay_verify_device with small entries
  *                           (the objects of 64- and 128-byte values): 1
  *                           (default) checks each object while its record is
@@ -509,9 +506,8 @@ int ramcrc_ctx_check(ramcrc_ctx* ctx, void* stream);
 /* Diagnostics.  ramcrc_ctx_debug_bins waits for the device and copies the
  * small-entry bin table's counts, both counter copies' cursors and
  * histograms (5 x 161 words), then the number of one-launch binnings that
- * aborted and completed through the two-launch path (1 word), the
- * speculation hint of RAMCRC_OPT_SPEC_TINY (1 word), to host, and the parity
- * of the next sequence. */
+ * aborted and completed through the two-launch path (1 word), to host, and
+ * the parity of the next sequence. */
 int ramcrc_ctx_debug_bins(ramcrc_ctx* ctx, uint64_t* host, uint64_t nwords, uint32_t* par_next);
 const char* ramcrc_strerror(int code);
 int ramcrc_last_hip_error(void);            /* last hipError_t seen (thread-local) */

@@ -185,21 +185,6 @@ int ramcrc_ctx_create(int device, ramcrc_ctx** out)
         return RAMCRC_ENOMEM;
     }
     (void)hipMemset(c->bins, 0, sizeof(BinTable));   // hist must start at zero
-    // the speculation hint (Sorted::hint): a host-mapped word the binning
-    // writes; without it the speculative pass runs only when forced
-    if (hipHostMalloc(reinterpret_cast<void**>(&c->spec_hint), 64,
-                      hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
-        *c->spec_hint = 0;
-        void* dp = nullptr;
-        if (hipHostGetDevicePointer(&dp, c->spec_hint, 0) == hipSuccess) {
-            c->spec_hint_dev = static_cast<uint32_t*>(dp);
-        } else {
-            (void)hipHostFree(c->spec_hint);
-            c->spec_hint = nullptr;
-        }
-    } else {
-        c->spec_hint = nullptr;
-    }
     *out = c;
     return RAMCRC_OK;
 }
@@ -232,7 +217,6 @@ int ramcrc_ctx_destroy(ramcrc_ctx* c)
     if (c->walk_left) (void)hipFree(c->walk_left);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
-    if (c->spec_hint) (void)hipHostFree(c->spec_hint);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->compute_stream) (void)hipStreamDestroy(c->compute_stream);
     for (auto& ev : c->ev_used) {
@@ -276,10 +260,8 @@ int ramcrc_ctx_set_option(ramcrc_ctx* c, int option, int64_t value)
     case RAMCRC_OPT_TEST_BIN_STRAGGLER:
         c->bin_straggler = value != 0;
         return RAMCRC_OK;
-    case RAMCRC_OPT_SPEC_TINY:
-        if (value < 0 || value > 2)
-            return RAMCRC_EINVAL;
-        c->spec_tiny = int(value);
+    case RAMCRC_OPT_BIN_ONE:
+        c->bin_one = value != 0;
         return RAMCRC_OK;
     case RAMCRC_OPT_VERIFY_IN_WALK:
         if (value < 0 || value > 2)
@@ -369,7 +351,7 @@ int ramcrc_ctx_debug_bins(ramcrc_ctx* c, uint64_t* host, uint64_t nwords, uint32
     DeviceGuard g(c->device);
     HIPCHK(hipDeviceSynchronize());
     // count[kNB], then cursor[0][kNB], cursor[1][kNB], then hist[0], hist[1] (as uint64),
-    // the k_bin_one rescues, the speculation hint
+    // the k_bin_one rescues
     std::vector<uint64_t> v;
     BinTable h;
     HIPCHK(hipMemcpy(&h, c->bins, sizeof(BinTable), hipMemcpyDeviceToHost));
@@ -379,7 +361,6 @@ int ramcrc_ctx_debug_bins(ramcrc_ctx* c, uint64_t* host, uint64_t nwords, uint32
     for (int p = 0; p < 2; p++)
         for (int b = 0; b < kNB; b++) v.push_back(h.ctr[p].hist[b]);
     v.push_back(h.rescues);
-    v.push_back(c->spec_hint ? __atomic_load_n(c->spec_hint, __ATOMIC_RELAXED) : 0u);
     for (uint64_t i = 0; i < nwords && i < v.size(); i++)
         host[i] = v[i];
     if (par_next)

@@ -34,7 +34,7 @@ OPT_WALK_PART_SHIFT = 2
 OPT_TEST_FAIL_AFTER_COUNT = 3
 OPT_TEST_DIRTY_BINS = 4
 OPT_TEST_BIN_STRAGGLER = 5
-OPT_SPEC_TINY = 6
+OPT_BIN_ONE = 6
 OPT_VERIFY_IN_WALK = 7
 
 
@@ -329,15 +329,6 @@ class Context:
         """One-launch binnings of this context that aborted (part of the grid
         not dispatched in time) and completed through the two-launch path."""
         buf = np.zeros(5 * 161 + 1, np.uint64)
-        par = _c.c_uint32(0)
-        _check(lib().ramcrc_ctx_debug_bins(self._h, _c.c_void_p(buf.ctypes.data), buf.size,
-                                           _c.byref(par)), "ramcrc_ctx_debug_bins")
-        return int(buf[-1])
-
-    def spec_hint(self):
-        """The speculation hint of this context (RAMCRC_OPT_SPEC_TINY): 1 when
-        its last small-entry table batch binned as all one-window entries."""
-        buf = np.zeros(5 * 161 + 2, np.uint64)
         par = _c.c_uint32(0)
         _check(lib().ramcrc_ctx_debug_bins(self._h, _c.c_void_p(buf.ctypes.data), buf.size,
                                            _c.byref(par)), "ramcrc_ctx_debug_bins")

@@ -72,7 +72,7 @@ VARIANTS = {
     "cu8": ["RAMCRC_COPY_U=8"],
     "tk5": ["RAMCRC_TINY_K=5"],
     "tk6": ["RAMCRC_TINY_K=6"],
-    "bo0": ["RAMCRC_BIN_ONE=0"],
+    "bo1": ["RAMCRC_BIN_ONE=1"],
     # round 5: tiny tables built in LDS from basis words (0 = copied from g_tab)
     "tg0": ["RAMCRC_TINY_GEN=0"],
     "hm0": ["RAMCRC_TINY_HM=0"],
@@ -97,8 +97,6 @@ VARIANTS = {
     "kap288": ["RAMCRC_SPLIT_KAPPA=288"],
     "bsp32": ["RAMCRC_BIN_SLEEP=32"],
     "cpf0": ["RAMCRC_COUNT_PF=0"],
-    # round 6: the speculative direct tiny pass off
-    "spec0": ["RAMCRC_SPEC_TINY=0"],
     # round 6: dense batches in 32 KiB parts, k_walk_parts keeping 32 records per lane in LDS
     "dense15": ["RAMCRC_PART_SHIFT_DENSE=15", "RAMCRC_PART_LREC=32"],
     "dense15a": ["RAMCRC_PART_SHIFT_DENSE=15", "RAMCRC_PART_LREC=32", "RAMCRC_SYNC_ADAPT=1"],

@@ -205,12 +205,13 @@ def test_direct_path_long_windows(ctx, ramcrc, oracle_mod, api):
 
 
 @pytest.mark.parametrize("api", ["entries", "batch"])
-def test_one_launch_threshold(ctx, oracle_mod, api):
+def test_one_launch_threshold(ctx, ramcrc, oracle_mod, api):
     """Batches either side of the one-launch binning limit (one 4,096-entry
     tile per 1,024-thread workgroup, one workgroup per CU -- half of the two a
     CU holds: 1,048,576 entries on 256 CUs)
     and a few small ones: k_bin_one and the two-launch path give the same,
     exact CRCs, with and without initial states."""
+    ctx.set_option(ramcrc.OPT_BIN_ONE, 1)   # (the default since round 6 is the two-launch path)
     rng = np.random.default_rng(5150)
     total = 4 << 20
     host = oracle_mod.splitmix_bytes(31, total)
@@ -239,6 +240,7 @@ def test_one_launch_binning_gives_up(ctx, ramcrc, oracle_mod, api):
     states, and counts one rescue."""
     host, offs, ls, init = alignment_case(oracle_mod, seed=13)
     base = dev(host)
+    ctx.set_option(ramcrc.OPT_BIN_ONE, 1)
     r0 = ctx.bin_rescues()
     for it in (init, None):
         ctx.set_option(ramcrc.OPT_TEST_BIN_STRAGGLER, 1)
@@ -253,7 +255,8 @@ def test_one_launch_binning_gives_up(ctx, ramcrc, oracle_mod, api):
     ctx.check()
 
 
-def test_concurrent_contexts_config3(ramcrc, oracle_mod):
+@pytest.mark.parametrize("bin_one", [0, 1])
+def test_concurrent_contexts_config3(ramcrc, oracle_mod, bin_one):
     """Four contexts on four streams, one host thread each (the deployment
     include/ramcrc.h prescribes: one context per launching thread; the
     reference replays from 1-16 threads, nanobenchmarks/RecoverSegmentBenchmark.cc:88-118),
@@ -273,6 +276,8 @@ def test_concurrent_contexts_config3(ramcrc, oracle_mod):
     len_t = dev(np.asarray(lens, dtype=np.uint64).view(np.int64))
     nctx, iters = 4, 6
     ctxs = [ramcrc.Context(0) for _ in range(nctx)]
+    for c in ctxs:
+        c.set_option(ramcrc.OPT_BIN_ONE, bin_one)
     streams = [torch.cuda.Stream() for _ in range(nctx)]
     outs = [[torch.zeros(len(lens), dtype=torch.int32, device="cuda") for _ in range(iters)]
             for _ in range(nctx)]
@@ -337,59 +342,3 @@ def test_long_phase_sparse_batches(ctx, oracle_mod):
             bad = np.nonzero(got != want)[0]
             assert bad.size == 0, (k, api, [(int(offs[i]) % 128, int(lens[i])) for i in bad[:8]])
     ctx.check()
-
-
-@pytest.mark.parametrize("api", ["entries", "batch"])
-@pytest.mark.parametrize("mode", [1, 2])
-def test_speculative_tiny_pass(ramcrc, oracle_mod, api, mode):
-    """The speculative direct tiny pass (RAMCRC_OPT_SPEC_TINY; 1: on the
-    hint the last all-tiny batch left, 2: always): the caller's table is
-    checksummed in place before any binning, and the binning and k_entries
-    behind it exit when every entry was tiny.  A sequence of batches on one
-    context where the speculation holds, fails in the first round of every
-    workgroup (the config-3 mix shape), fails late (one entry that is not
-    tiny, last in the table, so one wave finds it after its other rounds ran),
-    fails in the middle, and holds again; tiny batches at every alignment,
-    with and without initial states, raw and finalized.  Every CRC exact, the
-    hint following the batches."""
-    c = ramcrc.Context(0)
-    try:
-        c.set_option(ramcrc.OPT_SPEC_TINY, mode)
-        rng = np.random.default_rng(606 + mode)
-        host = oracle_mod.splitmix_bytes(66, 1 << 20)
-        base = dev(host)
-        n = 200_000
-        offs = rng.integers(0, (1 << 20) - 9000, n)
-        lens = rng.integers(0, 113, n)
-        offs[:2048] = 512 + np.arange(2048)              # every alignment
-        lens[:2048] = 128 - (offs[:2048] % 16)            # windows ending exactly at 128
-        lens[2048:2100] = np.arange(52) % 4               # bytewise entries
-        init = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
-        late = lens.copy()
-        late[-1] = 300
-        mid = lens.copy()
-        mid[n // 2] = 129
-        mix = lens.copy()
-        mix[::7] = 1500
-        seq = [("tiny", lens, None, 1), ("tiny+init", lens, init, 1), ("late", late, None, 0),
-               ("tiny", lens, init, 1), ("mix", mix, init, 0), ("tiny", lens, None, 1),
-               ("mid", mid, None, 0), ("tiny", lens, init, 1), ("tiny", lens, None, 1)]
-        for name, ls, it, hint in seq:
-            for fin in (True, False):
-                off_t = dev(np.asarray(offs, dtype=np.uint64).view(np.int64))
-                len_t = dev(np.asarray(ls, dtype=np.uint64).view(np.int64))
-                init_t = None if it is None else dev(np.asarray(it, dtype=np.uint32).view(np.int32))
-                out = torch.zeros(n, dtype=torch.int32, device="cuda")
-                getattr(c, api)(base, off_t, len_t, out, init=init_t, finalize=fin)
-                got = host_u32(out)
-                want = oracle_mod.entries(host, offs, ls, init=it, finalize=fin)
-                bad = np.nonzero(got != want)[0]
-                assert bad.size == 0, (name, fin, [(int(offs[i]) % 16, int(ls[i])) for i in bad[:8]])
-                assert c.spec_hint() == hint, (name, fin)
-        # a tiny batch smaller than one round of a wave, and a single entry
-        for k in (1, 37):
-            got = host_u32(run(c, api, base, offs[:k], lens[:k]))
-            assert np.array_equal(got, oracle_mod.entries(host, offs[:k], lens[:k]))
-        c.check()
-    finally:
-        c.close()
