@@ -847,7 +847,10 @@ int walk_impl(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride, uint32_t s
             uint64_t gv = (total + kVWaves - 1) / kVWaves;   // a wave per part
             if (gv > uint64_t(16) * c->ncu)
                 gv = uint64_t(16) * c->ncu;
-            hipLaunchKernelGGL(k_walk_copyv, dim3(gv), dim3(kVWaves * kWaveSize), 0, s, pw);
+            // (the probe picks the stage size; the other instantiation exits)
+            hipLaunchKernelGGL(k_walk_copyv<kVStageS>, dim3(gv), dim3(kVWaves * kWaveSize), 0, s, pw);
+            HIPCHK(hipGetLastError());
+            hipLaunchKernelGGL(k_walk_copyv<kVStageL>, dim3(gv), dim3(kVWaves * kWaveSize), 0, s, pw);
             HIPCHK(hipGetLastError());
         }
         w.only = c->walk_fallback;

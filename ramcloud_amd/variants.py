@@ -97,17 +97,6 @@ VARIANTS = {
     "kap288": ["RAMCRC_SPLIT_KAPPA=288"],
     "bsp32": ["RAMCRC_BIN_SLEEP=32"],
     "cpf0": ["RAMCRC_COUNT_PF=0"],
-    # round 6: dense batches in 32 KiB parts, k_walk_parts keeping 32 records per lane in LDS
-    "dense15": ["RAMCRC_PART_SHIFT_DENSE=15", "RAMCRC_PART_LREC=32"],
-    "dense15a": ["RAMCRC_PART_SHIFT_DENSE=15", "RAMCRC_PART_LREC=32", "RAMCRC_SYNC_ADAPT=1"],
-    "sada": ["RAMCRC_SYNC_ADAPT=1"],
-    "lrec32": ["RAMCRC_PART_LREC=32"],
-    "vf0": ["RAMCRC_VFAST=0"],
-    # round 6: k_walk_copyv's byte tables in 8 / 16 copies (fewer LDS bank conflicts)
-    "vrep8": ["RAMCRC_VREP=8", "RAMCRC_VWAVES=8"],
-    "vrep16": ["RAMCRC_VREP=16", "RAMCRC_VWAVES=6"],
-    # round 6: k_walk_copyv's CRC by VALU bit-matrix (1) or half tables, half VALU (2)
-    "vcrc1": ["RAMCRC_VCRC=1"],
-    "vcrc2": ["RAMCRC_VCRC=2"],
-    "vcrc2r8": ["RAMCRC_VCRC=2", "RAMCRC_VREP=8", "RAMCRC_VWAVES=8"],
+    # round 6: k_walk_sync's stage always 7 KiB (the default sizes it from the mean entry)
+    "sada0": ["RAMCRC_SYNC_ADAPT=0"],
 }
