@@ -342,3 +342,51 @@ def test_long_phase_sparse_batches(ctx, oracle_mod):
             bad = np.nonzero(got != want)[0]
             assert bad.size == 0, (k, api, [(int(offs[i]) % 128, int(lens[i])) for i in bad[:8]])
     ctx.check()
+
+
+@pytest.mark.parametrize("api", ["entries", "batch"])
+def test_two_window_table_direct_path(ctx, ramcrc, oracle_mod, api):
+    """Table batches whose every entry spans exactly two 128-byte windows
+    (1M x 160 B log entries; here 129 .. 256-byte spans at every start
+    alignment) take the direct multi-window path: nothing is scattered and the
+    two-window ring reads the caller's (off, len, init) in place.  Exact with
+    and without initial states, raw and finalized, on both binning launches;
+    then a batch with one three-window entry (the layout switches back) and
+    the two-window batch again."""
+    rng = np.random.default_rng(2626)
+    total = 2 << 20
+    host = oracle_mod.splitmix_bytes(262, total)
+    base = dev(host)
+    n = 60000
+    offs = rng.integers(0, total - 512, n)
+    lens = rng.integers(100, 257, n)
+    a = offs & 15
+    keep = (a + lens > 128) & (a + lens <= 256)
+    offs, lens = offs[keep], lens[keep]
+    offs[:256] = 4096 + np.arange(256)                 # every alignment
+    lens[:256] = 256 - (offs[:256] % 16)               # ending exactly at the second window's end
+    lens[256:512] = 129 - (offs[256:512] % 16)         # one byte into the second window
+    init = rng.integers(0, 2 ** 32, offs.size, dtype=np.uint64).astype(np.uint32)
+    for one in (0, 1):
+        ctx.set_option(ramcrc.OPT_BIN_ONE, one)
+        for it in (None, init):
+            for fin in (True, False):
+                off_t = dev(np.asarray(offs, dtype=np.uint64).view(np.int64))
+                len_t = dev(np.asarray(lens, dtype=np.uint64).view(np.int64))
+                init_t = None if it is None else dev(np.asarray(it, dtype=np.uint32).view(np.int32))
+                out = torch.zeros(offs.size, dtype=torch.int32, device="cuda")
+                getattr(ctx, api)(base, off_t, len_t, out, init=init_t, finalize=fin)
+                got = host_u32(out)
+                want = oracle_mod.entries(host, offs, lens, init=it, finalize=fin)
+                bad = np.nonzero(got != want)[0]
+                assert bad.size == 0, (one, fin, [(int(offs[i]) % 16, int(lens[i])) for i in bad[:8]])
+        # the shortcut was taken: the layout holds no slot
+        count, _, _, _ = ctx.debug_bins()
+        assert int(count.sum()) == 0
+        lens3 = lens.copy()
+        lens3[offs.size // 2] = 300
+        got = host_u32(run(ctx, api, base, offs, lens3))
+        assert np.array_equal(got, oracle_mod.entries(host, offs, lens3))
+        got = host_u32(run(ctx, api, base, offs, lens, init))
+        assert np.array_equal(got, oracle_mod.entries(host, offs, lens, init=init))
+    ctx.check()
