@@ -99,6 +99,4 @@ VARIANTS = {
     "cpf0": ["RAMCRC_COUNT_PF=0"],
     # round 6: k_walk_sync's stage always 7 KiB (the default sizes it from the mean entry)
     "sada0": ["RAMCRC_SYNC_ADAPT=0"],
-    # round 6: k_walk_copyv's X^4 step through conflict-free nibble tables
-    "vnib": ["RAMCRC_VNIB=1"],
 }
