@@ -99,6 +99,4 @@ VARIANTS = {
     "cpf0": ["RAMCRC_COUNT_PF=0"],
     # round 6: k_walk_sync's stage always 7 KiB (the default sizes it from the mean entry)
     "sada0": ["RAMCRC_SYNC_ADAPT=0"],
-    # round 6: the part walk checks the objects itself (k_walk_partsv)
-    "walkv": ["RAMCRC_WALKV=1"],
 }
