@@ -99,4 +99,6 @@ VARIANTS = {
     "cpf0": ["RAMCRC_COUNT_PF=0"],
     # round 6: k_walk_sync's stage always 7 KiB (the default sizes it from the mean entry)
     "sada0": ["RAMCRC_SYNC_ADAPT=0"],
+    # round 6: A's header peek as one aligned 16-byte load (+ a dword for 1 hop in 4)
+    "p16": ["RAMCRC_PEEK16=1"],
 }

@@ -1,0 +1,14 @@
+# Round 6: A's header peek as one aligned 16-byte load (p16, RAMCRC_PEEK16)
+# against two dword loads: walk / replay / certify tests and a 64 B trace
+# under p16, replay A/B.
+set -o pipefail
+export TMPDIR=/tmp PYTHONUNBUFFERED=1
+O=gpurun_out/r06/${1:-p16}
+mkdir -p $O
+RAMCRC_LIB=ramcloud_amd/lib/variants/libramcrc_p16.so timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
+    tests/test_gpu_replay_fused.py tests/test_gpu_segments.py tests/test_gpu_segment_ref.py tests/test_gpu_certify.py \
+    -m gpu > $O/pytest.log 2>&1 || exit 1
+VARIANTS="p16" CASES="--config replay --value-len 64;--config replay --value-len 128;--config replay --value-len 256;--config replay --value-len 1024" \
+  REPS=2 STEPS=10 TAG=r06/${1:-p16}/ab bash tools/gpu_ab.sh || exit 1
+RAMCRC_LIB=ramcloud_amd/lib/variants/libramcrc_p16.so timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o r64 -- \
+    python3 bench.py --config replay --value-len 64 --steps 10 --no-cpu-baseline > $O/prof64.json 2>> $O/err.txt || exit 1
