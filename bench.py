@@ -818,7 +818,9 @@ def run_replay(args, ranks):
     ctx.close()
     scan_s = scan_ms / args.steps / 1e3
     achieved = obj_bytes / scan_s / 1e9 if scan_s > 0 else None
-    tkey = f"replay_{nseg}x{args.seg_mib}MiB_v{args.value_len}_k_entries"
+    # the object checks: k_entries, or k_walk_copyv in verify-in-walk mode
+    # (the timer brackets both, the idle one exits at once: 5-10 us)
+    tkey = f"replay_{nseg}x{args.seg_mib}MiB_v{args.value_len}_verify"
     return {
         "metric": "device-resident recovery replay verify GB/s of 8 MiB object segments "
                   "(segment walk + per-object checksum compare)",
@@ -837,7 +839,9 @@ def run_replay(args, ranks):
                             if args.walk_part_shift else
                             "parallel (part size from the entry density, k_walk_probe)"),
                    "objects": int(counts.sum()), "object_bytes_checksummed": obj_bytes},
-        "roofline": {"bound": "hbm", "kernel": "k_entries (object verify)",
+        "roofline": {"bound": "hbm",
+                     "kernel": "object verify (k_entries, or k_walk_copyv in verify-in-walk mode; "
+                               "the launches of both summed)",
                      "achieved": round(achieved, 1) if achieved else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,

@@ -463,8 +463,9 @@ int ramcrc_assemble_objects_host(ramcrc_ctx* ctx, void* const* objs, const uint6
 int ramcrc_ctx_set_option(ramcrc_ctx* ctx, int option, int64_t value);
 
 /* Kernel timing (for benchmarks): when enabled, every launch brackets its
- * byte-scan kernel (k_chunks, or k_entries on the small path) with HIP events
- * on the launch stream.  ramcrc_ctx_scan_time waits for the recorded events,
+ * byte-scan kernel (k_chunks, or k_entries on the small path; in the fused
+ * replay call also the two k_walk_copyv launches, which do the object checks
+ * in verify-in-walk mode) with HIP events on the launch stream.  ramcrc_ctx_scan_time waits for the recorded events,
  * returns the summed kernel milliseconds and the number of bracketed launches
  * since the last call, and resets both. */
 int ramcrc_ctx_set_timing(ramcrc_ctx* ctx, int enable);

@@ -101,4 +101,8 @@ VARIANTS = {
     "sada0": ["RAMCRC_SYNC_ADAPT=0"],
     # round 6: A's header peek as one aligned 16-byte load (+ a dword for 1 hop in 4)
     "p16": ["RAMCRC_PEEK16=1"],
+    # round 6: A with staged windows on verify-in-walk batches (k_walk_partsw)
+    "awin": ["RAMCRC_PARTS_WIN=1"],
+    # ... and checking the objects from its windows (k_walk_copy takes the CRCs)
+    "awinv": ["RAMCRC_PARTS_WIN=2"],
 }

@@ -16,7 +16,8 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = {"k_chunks": "k_chunks<", "k_entries": "k_entries("}
+KERNEL = {"k_chunks": "k_chunks<", "k_entries": "k_entries(",
+          "object verify": "k_entries(,k_walk_copyv<8192u>,k_walk_copyv<12288u>"}
 
 
 def main(out, keep):
