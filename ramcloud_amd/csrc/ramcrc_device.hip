@@ -215,8 +215,6 @@ int ramcrc_ctx_destroy(ramcrc_ctx* c)
     if (c->walk_pool_used) (void)hipFree(c->walk_pool_used);
     if (c->walk_sum) (void)hipFree(c->walk_sum);
     if (c->walk_left) (void)hipFree(c->walk_left);
-    if (c->walk_rcrc) (void)hipFree(c->walk_rcrc);
-    if (c->walk_pcrc) (void)hipFree(c->walk_pcrc);
     if (c->d_stage) (void)hipFree(c->d_stage);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -792,13 +790,6 @@ int walk_impl(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride, uint32_t s
         if (!rc && d_obj_crc && sum)
             rc = grow_device(reinterpret_cast<void**>(&c->walk_left), &c->walk_left_cap, left_cap,
                              sizeof(uint32_t));
-        // the windowed part walk that checks the objects (RAMCRC_PARTS_WIN 2):
-        // a {crc, state} beside every scratch and pool record slot
-        const bool walkv = RAMCRC_PARTS_WIN == 2 && d_obj_crc && sum;
-        if (!rc && walkv)
-            rc = grow_device(&c->walk_rcrc, &c->walk_rcrc_cap, total * kPartRec, sizeof(uint2));
-        if (!rc && walkv)
-            rc = grow_device(&c->walk_pcrc, &c->walk_pcrc_cap, pool_blocks * kPartRec, sizeof(uint2));
         if (rc)
             return rc;
         PWalk pw{};
@@ -831,10 +822,6 @@ int walk_impl(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride, uint32_t s
             pw.nleft = c->walk_pool_used + 2;
             pw.left_cap = left_cap;
             pw.vmode = uint32_t(c->verify_in_walk);
-            if (walkv) {
-                pw.rcrc = static_cast<uint2*>(c->walk_rcrc);
-                pw.pcrc = static_cast<uint2*>(c->walk_pcrc);
-            }
         }
         hipLaunchKernelGGL(k_walk_probe, dim3(1), dim3(kWaveSize), 0, s, pw, c->walk_pshift, geo);
         HIPCHK(hipGetLastError());
@@ -847,10 +834,6 @@ int walk_impl(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride, uint32_t s
         }
         hipLaunchKernelGGL(k_walk_parts, dim3((total + 255) / 256), dim3(256), 0, s, pw);
         HIPCHK(hipGetLastError());
-        if (RAMCRC_PARTS_WIN && pw.obj_crc) {   // (one of the two part walks exits)
-            hipLaunchKernelGGL(k_walk_partsw, dim3((total + 255) / 256), dim3(256), 0, s, pw);
-            HIPCHK(hipGetLastError());
-        }
         hipLaunchKernelGGL(k_walk_fix, dim3(grid), dim3(kWaveSize), 0, s, pw);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_walk_emit, dim3((total + 255) / 256), dim3(256), 0, s, pw);

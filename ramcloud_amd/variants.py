@@ -99,10 +99,4 @@ VARIANTS = {
     "cpf0": ["RAMCRC_COUNT_PF=0"],
     # round 6: k_walk_sync's stage always 7 KiB (the default sizes it from the mean entry)
     "sada0": ["RAMCRC_SYNC_ADAPT=0"],
-    # round 6: A's header peek as one aligned 16-byte load (+ a dword for 1 hop in 4)
-    "p16": ["RAMCRC_PEEK16=1"],
-    # round 6: A with staged windows on verify-in-walk batches (k_walk_partsw)
-    "awin": ["RAMCRC_PARTS_WIN=1"],
-    # ... and checking the objects from its windows (k_walk_copy takes the CRCs)
-    "awinv": ["RAMCRC_PARTS_WIN=2"],
 }

@@ -1,6 +1,6 @@
-# Round 6: A's LDS record rows rotated per lane (default) against the
-# round-5 layout (lrot0): walk/replay tests on the tree, replay A/B, and an
-# LDS bank-conflict pass over the 64 B replay.
+# Round 6: the part walk's LDS record rows rotated per lane: walk/replay tests,
+# replay A/B against lrot0 (a knob removed afterwards; its build was wrong,
+# so the A/B is void) and the LDS bank-conflict pass (pmc_summary.txt).
 set -o pipefail
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 O=gpurun_out/r06/${1:-lrot}
