@@ -137,6 +137,43 @@ def test_fused_multi_window_direct(ramcrc, vlen):
         ctx.close()
 
 
+@pytest.mark.parametrize("viw", [0, 1])
+def test_fused_mixed_two_and_three_window_values(ramcrc, viw):
+    """One batch of 128 B-value segments (two-window objects) and 256 B-value
+    segments (three windows): the summary must send it to the general
+    multi-window loop, not the two-window ring, which reads only two windows
+    (the in-place check refuses k > kK).  With and without verify-in-walk:
+    identical to the split calls, one damaged object in each half."""
+    from ramcloud_amd import segments
+    half = 6
+    nseg = 2 * half
+    ctx = ramcrc.Context(0)
+    ctx.set_option(ramcrc.OPT_VERIFY_IN_WALK, viw)
+    try:
+        d = torch.empty(nseg * SEG, dtype=torch.uint8, device="cuda")
+        certs = torch.zeros((nseg, 2), dtype=torch.int32, device="cuda")
+        lo, hi = d[:half * SEG], d[half * SEG:]
+        from ramcloud_amd import workloads
+        workloads.splitmix_fill_segments(d, SEG, 0x2563)
+        p128, _, _ = ctx.fill_objects(lo, SEG, SEG, half, 128, first_key=0, certs=certs[:half])
+        p256, _, _ = ctx.fill_objects(hi, SEG, SEG, half, 256, first_key=0, certs=certs[half:])
+        torch.cuda.synchronize()
+        e128, e256 = segments.entry_bytes(128), segments.entry_bytes(256)
+        d[1 * SEG + 77 * e128 + e128 - 5] ^= 0x10   # value bytes (as above)
+        d[(half + 2) * SEG + 91 * e256 + e256 - 5] ^= 0x01
+        cap = half * (p128 + p256) + 1024
+        fs, fn, ft, fc = _run(ramcrc, ctx, d, certs, nseg, cap, fused=True)
+        ss, sn, st, sc = _run(ramcrc, ctx, d, certs, nseg, cap, fused=False)
+        assert fn == sn == half * (p128 + p256)
+        assert np.array_equal(fs, ss) and np.array_equal(ft, st) and np.array_equal(fc, sc)
+        assert (fs[:, 0] == segments.SEG_OK).all()
+        bad = np.zeros(nseg, np.uint32)
+        bad[1] = bad[half + 2] = 1
+        assert np.array_equal(fs[:, 3], bad)
+    finally:
+        ctx.close()
+
+
 def _hist_empty(ctx, n):
     """The verify-in-walk mode was taken: the binned verify's count pass
     exited with an empty histogram although the table holds n records."""
