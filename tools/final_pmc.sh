@@ -18,3 +18,8 @@ run e100 --config entries --entry-size 100 || exit 1
 run append --config append || exit 1
 run replay --config replay || exit 1
 run replay64 --config replay --value-len 64 || exit 1
+run replay128 --config replay --value-len 128 || exit 1
+run replay256 --config replay --value-len 256 || exit 1
+run replay8192 --config replay --value-len 8192 || exit 1
+run e1024 --config entries --entry-size 1024 || exit 1
+run e4096 --config entries --entry-size 4096 || exit 1
