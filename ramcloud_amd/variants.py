@@ -99,4 +99,6 @@ VARIANTS = {
     "cpf0": ["RAMCRC_COUNT_PF=0"],
     # round 6: k_walk_sync's stage always 7 KiB (the default sizes it from the mean entry)
     "sada0": ["RAMCRC_SYNC_ADAPT=0"],
+    # round 6: the probe may pick 128 KiB parts again (entries of ~1.45 .. 2.9 KiB)
+    "p17": ["RAMCRC_SKIP_P17=0"],
 }
