@@ -823,6 +823,17 @@ int walk_impl(ramcrc_ctx* c, const void* d_base, uint64_t seg_stride, uint32_t s
             pw.left_cap = left_cap;
             pw.vmode = uint32_t(c->verify_in_walk);
         }
+        // The pool block map starts empty on every call: the part -> block
+        // table (blocks) and the block -> part table (pool_owner) of the
+        // previous call on this context are stale, and the fix-up's block
+        // replacement reads them.  Carried over, they gave wrong records on a
+        // repeated call when the fix-up re-walked parts with pool blocks
+        // (replay of 2 and 3 KiB values, 256 KiB parts: records of one part's
+        // pool block replaced by another's, found in round 6 by the bench's
+        // object-CRC check, tests/test_gpu_replay_fused.py::
+        // test_repeated_calls_pool_blocks).
+        HIPCHK(hipMemsetAsync(c->walk_blocks, 0xFF, total * kMaxBlocks * sizeof(uint32_t), s));
+        HIPCHK(hipMemsetAsync(c->walk_pool_owner, 0xFF, pool_blocks * sizeof(uint32_t), s));
         hipLaunchKernelGGL(k_walk_probe, dim3(1), dim3(kWaveSize), 0, s, pw, c->walk_pshift, geo);
         HIPCHK(hipGetLastError());
         if (nparts > 1) {

@@ -283,3 +283,43 @@ def test_verify_in_walk_replay_mix(ramcrc, oracle_mod, golden):
     for k in range(3):
         assert np.array_equal(got[2][k], got[0][k]), k
     assert np.array_equal(got[2][0][:, 3], bad_exp) and int(bad_exp.sum()) > 0
+
+
+@pytest.mark.parametrize("vlen", [2048, 3072])
+def test_repeated_calls_pool_blocks(ramcrc, oracle_mod, vlen):
+    """The same batch verified four times on one context, as a replay thread
+    does batch after batch: 2 and 3 KiB values walk in 256 KiB parts of 83 ..
+    125 entries, so parts keep records in pool blocks and the fix-up re-walks
+    some of them.  Every call's records and object CRCs equal the first call's
+    and, for the first segments, the oracle's walk (round 6: a block map kept
+    from the previous call replaced one part's pool block by another's)."""
+    from ramcloud_amd import segments
+    nseg, check = 256, 6
+    ctx = ramcrc.Context(0)
+    try:
+        d, certs, per, ck = _batch(ramcrc, ctx, nseg, vlen, first_seed=0x3C3C + vlen)
+        host = d[:check * SEG].cpu().numpy()
+        cn = certs.cpu().numpy().view(np.uint32)
+        want = np.concatenate([oracle_mod.check_metadata(host[s * SEG:(s + 1) * SEG], int(cn[s, 0]),
+                                                         int(cn[s, 1]), segment=s, capacity=SEG)[3]
+                               for s in range(check)])
+        rv = segments.RecoveryVerify(ctx, nseg, SEG, entries_cap=nseg * per + nseg)
+        first = None
+        for call in range(4):
+            st = rv.verify(d, certs, check=True)
+            torch.cuda.synchronize()
+            n = int(rv.n_entries.item())
+            t = rv.entries[:n].cpu().numpy().view(np.uint32).reshape(-1, 4)
+            c = rv.obj_crc[:n].cpu().numpy().view(np.uint32)
+            o = np.lexsort((t[:, 1], t[:, 0]))
+            t, c = t[o], c[o]
+            s = st.cpu().numpy().view(np.uint32)
+            assert (s[:, 0] == segments.SEG_OK).all() and (s[:, 3] == 0).all(), call
+            assert n == nseg * per, call
+            assert np.array_equal(t[t[:, 0] < check], want), call
+            if first is None:
+                first = (t, c)
+            else:
+                assert np.array_equal(t, first[0]) and np.array_equal(c, first[1]), call
+    finally:
+        ctx.close()

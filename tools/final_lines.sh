@@ -21,7 +21,7 @@ timeout -k 10 200 python bench.py --config append > "$OUT/append.json" 2> "$OUT/
 timeout -k 10 300 python bench.py --config stream > "$OUT/stream.json" 2> "$OUT/stream.err" || exit 1
 fi
 if [[ $PART == *b* ]]; then
-for v in 64 128 256 512 1024 2048 8192; do
+for v in 64 128 256 512 1024 2048 3072 4096 8192; do
   timeout -k 10 200 python bench.py --config replay --value-len $v > "$OUT/replay_$v.json" 2> "$OUT/replay_$v.err" || exit 1
 done
 timeout -k 10 200 python bench.py --config replay > "$OUT/replay.json" 2> "$OUT/replay.err" || exit 1
