@@ -11,6 +11,10 @@ run() {   # name, bench arguments...
   timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/$n" -o p -- \
       python3 bench.py "$@" --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/$n.json" 2> "$OUT/$n.err"
 }
+if [ -n "$EXTRA" ]; then   # only the replay sizes added in round 6
+  for v in 512 2048 3072 4096; do run replay$v --config replay --value-len $v || exit 1; done
+  exit 0
+fi
 run c2 || exit 1
 run c4 --config recovery --no-t1 || exit 1
 run mix --config entries || exit 1
