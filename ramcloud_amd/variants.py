@@ -101,4 +101,6 @@ VARIANTS = {
     "sada0": ["RAMCRC_SYNC_ADAPT=0"],
     # round 6: the probe may pick 128 KiB parts again (entries of ~1.45 .. 2.9 KiB)
     "p17": ["RAMCRC_SKIP_P17=0"],
+    # round 6: role split off with a heavier octet cost (the long-phase re-check)
+    "sp0oc6": ["RAMCRC_SPLIT=0", "RAMCRC_OCTET_COST=6"],
 }
