@@ -20,7 +20,8 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
             if r["Counter_Name"] == c:
                 k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
                 per[k].append(float(r["Counter_Value"]) * 1024 * (2 if c == "FETCH_SIZE" else 1))
-    tot[c] = {k: sum(v[-steps:]) / steps for k, v in per.items() if k.startswith("k_")}
+    # kernels of the step run at least `steps` times; the fill's run once
+    tot[c] = {k: sum(v[-steps:]) / steps for k, v in per.items() if k.startswith("k_") and len(v) >= steps}
 ks = sorted(set(tot["FETCH_SIZE"]) | set(tot["WRITE_SIZE"]), key=lambda k: -tot["FETCH_SIZE"].get(k, 0))
 print(f"{tag}: per step, GB (FETCH_SIZE x 2 | WRITE_SIZE)")
 fr = wr = 0
